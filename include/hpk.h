@@ -1,0 +1,121 @@
+/*
+ * hpk.h — C ABI of the MI355X-native HPACK Huffman codec (RFC 7541 §5.2 + App. B).
+ *
+ * This is the drop-in boundary for loona-hpack's Huffman string-literal path.
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, never
+ * throws across the boundary and never panics on input bytes.
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * bearcove/loona @ 2025-05-09):
+ *
+ *   hpk_huffman_decode_one   HuffmanDecoder::new().decode(buf)
+ *                            crates/loona-hpack/src/huffman.rs:86-88, :95-161
+ *                            called from decode_string, crates/loona-hpack/src/decoder.rs:148-149
+ *   hpk_status               HuffmanDecoderError {PaddingTooLarge, InvalidPadding, EOSInString}
+ *                            crates/loona-hpack/src/huffman.rs:28-41 (1:1 mapping, 0 = Ok)
+ *   hpk_decode_batch         many decode_string Huffman branches at once
+ *                            (decoder.rs:143-157), literals gathered across header blocks /
+ *                            streams by the caller (crates/loona/src/h2/server.rs:1619-1638)
+ *   hpk_huffman_encode_one   NEW: the reference never Huffman-encodes
+ *   hpk_encode_batch         (crates/loona-hpack/src/encoder.rs:296-307 writes raw literals);
+ *                            this is the H-bit branch encode_string_literal would add.
+ *
+ * Threading: one hpk_ctx per host thread (loona is !Send, thread-per-core,
+ * crates/buffet/src/lib.rs:38-49). A context owns a HIP stream (or borrows
+ * one via hpk_ctx_set_stream) and grow-only device scratch buffers.
+ */
+#ifndef HPK_H
+#define HPK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-literal status (one byte per literal in batch calls) ---------- */
+typedef enum hpk_status {
+    HPK_OK = 0,                 /* Ok(Vec<u8>)                                 */
+    HPK_PADDING_TOO_LARGE = 1,  /* HuffmanDecoderError::PaddingTooLarge  (>7 residual bits) */
+    HPK_INVALID_PADDING = 2,    /* HuffmanDecoderError::InvalidPadding   (residual != EOS MSBs) */
+    HPK_EOS_IN_STRING = 3,      /* HuffmanDecoderError::EOSInString      (30-bit EOS decoded) */
+    HPK_OUTPUT_OVERFLOW = 4     /* not a reference error: caller's out capacity < decoded size */
+} hpk_status;
+
+/* ---- API return codes (negative = the call itself failed) -------------- */
+#define HPK_E_OK 0
+#define HPK_E_INVAL (-1)    /* bad argument (null pointer, offsets not monotone, ...) */
+#define HPK_E_NOSPACE (-2)  /* single-literal call: `cap` too small               */
+#define HPK_E_DEVICE (-3)   /* HIP runtime error; see hpk_last_error()            */
+#define HPK_E_NODEVICE (-4) /* no GPU / kernel image for gfx950 not loadable      */
+
+/* ---- flags for batch calls --------------------------------------------- */
+#define HPK_PTR_HOST 0x0   /* all buffers are host memory: stage H2D, run, D2H, sync  */
+#define HPK_PTR_DEVICE 0x1 /* all buffers are device memory: enqueue on the ctx stream */
+#define HPK_ASYNC 0x2      /* with HPK_PTR_DEVICE: return without synchronising       */
+
+/* Upper bounds for output capacity. Every HPACK code is >= 5 bits and <= 30 bits. */
+size_t hpk_decoded_bound(size_t encoded_len); /* floor(8n/5)    */
+size_t hpk_encoded_bound(size_t decoded_len); /* ceil(30n/8)    */
+
+/* Canonical Huffman encoded length of `in` (bytes, incl. EOS-prefix padding). */
+size_t hpk_huffman_encoded_len(const uint8_t* in, size_t n);
+
+/* ---- single-literal CPU entry points (the scalar drop-in) --------------- */
+/* Decode n bytes. Returns an hpk_status (>= 0) and sets *out_len to the number
+ * of bytes written (also on error: the symbols decoded before the error), or a
+ * negative HPK_E_* code. `out` may be NULL iff cap == 0. */
+int hpk_huffman_decode_one(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+
+/* Encode n bytes (MSB-first codes, padded with the most significant bits of
+ * EOS). Returns HPK_E_OK or HPK_E_NOSPACE. */
+int hpk_huffman_encode_one(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+
+/* ---- device context ----------------------------------------------------- */
+typedef struct hpk_ctx hpk_ctx;
+
+hpk_ctx* hpk_ctx_create(int device);           /* NULL on failure (see hpk_last_error(NULL)) */
+void hpk_ctx_destroy(hpk_ctx* ctx);
+int hpk_ctx_set_stream(hpk_ctx* ctx, void* hip_stream); /* NULL = the ctx's own stream */
+void* hpk_ctx_stream(hpk_ctx* ctx);
+int hpk_ctx_sync(hpk_ctx* ctx);
+const char* hpk_last_error(const hpk_ctx* ctx); /* thread-local text of the last failure */
+
+/* ---- batch decode --------------------------------------------------------
+ * Literal i occupies in_blob[in_off[i] .. in_off[i+1]) and may write
+ * out_blob[out_off[i] .. out_off[i+1]) (its capacity; hpk_decoded_bound of
+ * its length always suffices). On return out_len[i] = bytes decoded and
+ * status[i] = hpk_status. Bytes of a literal's region past out_len[i] are
+ * unspecified. Offsets are u32 (one shard < 4 GiB); in_off/out_off have n+1
+ * entries and must be non-decreasing. */
+int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
+                     uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len,
+                     uint8_t* status, int flags);
+
+/* ---- batch encode --------------------------------------------------------
+ * Symmetric: literal i = in_blob[in_off[i] .. in_off[i+1]) is Huffman-encoded
+ * into out_blob[out_off[i] ..) with capacity out_off[i+1]-out_off[i]
+ * (hpk_encoded_bound suffices). out_len[i] = encoded bytes; status[i] is
+ * HPK_OK or HPK_OUTPUT_OVERFLOW. */
+int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
+                     uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len,
+                     uint8_t* status, int flags);
+
+/* ---- batch calls on the host CPU ----------------------------------------
+ * Same layout and results as the device calls, run by `nthreads` host threads over contiguous
+ * literal shards balanced by bytes (thread-per-core, like loona). This is the table-driven CPU
+ * path ("cpu-fast" in the bench), not the reference restatement. nthreads <= 0: all cores. */
+int hpk_decode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
+                         const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int nthreads);
+int hpk_encode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
+                         const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int nthreads);
+
+/* Library/kernel identification (for logs and the bench JSON). */
+const char* hpk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HPK_H */

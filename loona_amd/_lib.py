@@ -1,0 +1,119 @@
+"""ctypes binding of libhpk.so (the C ABI in include/hpk.h).
+
+The library is built in-tree (loona_amd/libhpk.so, by __graft_entry__.build() or
+`make -C loona_amd/csrc`). There is no fallback: if the library is missing or does not load,
+every entry point raises, so a GPU run can never silently take a CPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HPK_LIB", os.path.join(HERE, "libhpk.so"))
+
+# hpk_status (hpk.h) <-> HuffmanDecoderError (crates/loona-hpack/src/huffman.rs:28-41)
+HPK_OK = 0
+HPK_PADDING_TOO_LARGE = 1
+HPK_INVALID_PADDING = 2
+HPK_EOS_IN_STRING = 3
+HPK_OUTPUT_OVERFLOW = 4
+
+HPK_E_OK = 0
+HPK_E_INVAL = -1
+HPK_E_NOSPACE = -2
+HPK_E_DEVICE = -3
+HPK_E_NODEVICE = -4
+
+HPK_PTR_HOST = 0x0
+HPK_PTR_DEVICE = 0x1
+HPK_ASYNC = 0x2
+
+# every symbol include/hpk.h declares (tests/test_host.py checks the .so exports all of them)
+EXPORTS = (
+    "hpk_decoded_bound",
+    "hpk_encoded_bound",
+    "hpk_huffman_encoded_len",
+    "hpk_huffman_decode_one",
+    "hpk_huffman_encode_one",
+    "hpk_ctx_create",
+    "hpk_ctx_destroy",
+    "hpk_ctx_set_stream",
+    "hpk_ctx_stream",
+    "hpk_ctx_sync",
+    "hpk_last_error",
+    "hpk_decode_batch",
+    "hpk_encode_batch",
+    "hpk_decode_batch_cpu",
+    "hpk_encode_batch_cpu",
+    "hpk_version",
+)
+
+_lock = threading.Lock()
+_lib = None
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_sizep = ctypes.POINTER(ctypes.c_size_t)
+
+
+def lib() -> ctypes.CDLL:
+    """Load libhpk.so once; raise (never fall back) if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libhpk.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                " or `make -C loona_amd/csrc` (there is no CPU fallback)"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        L.hpk_decoded_bound.argtypes = [ctypes.c_size_t]
+        L.hpk_decoded_bound.restype = ctypes.c_size_t
+        L.hpk_encoded_bound.argtypes = [ctypes.c_size_t]
+        L.hpk_encoded_bound.restype = ctypes.c_size_t
+        L.hpk_huffman_encoded_len.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.hpk_huffman_encoded_len.restype = ctypes.c_size_t
+        for fn in (L.hpk_huffman_decode_one, L.hpk_huffman_encode_one):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, c_sizep]
+            fn.restype = ctypes.c_int
+        L.hpk_ctx_create.argtypes = [ctypes.c_int]
+        L.hpk_ctx_create.restype = ctypes.c_void_p
+        L.hpk_ctx_destroy.argtypes = [ctypes.c_void_p]
+        L.hpk_ctx_destroy.restype = None
+        L.hpk_ctx_set_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.hpk_ctx_set_stream.restype = ctypes.c_int
+        L.hpk_ctx_stream.argtypes = [ctypes.c_void_p]
+        L.hpk_ctx_stream.restype = ctypes.c_void_p
+        L.hpk_ctx_sync.argtypes = [ctypes.c_void_p]
+        L.hpk_ctx_sync.restype = ctypes.c_int
+        L.hpk_last_error.argtypes = [ctypes.c_void_p]
+        L.hpk_last_error.restype = ctypes.c_char_p
+        for fn in (L.hpk_decode_batch, L.hpk_encode_batch):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+            fn.restype = ctypes.c_int
+        for fn in (L.hpk_decode_batch_cpu, L.hpk_encode_batch_cpu):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+            fn.restype = ctypes.c_int
+        L.hpk_version.argtypes = []
+        L.hpk_version.restype = ctypes.c_char_p
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    msg = lib().hpk_last_error(None)
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+    return rc

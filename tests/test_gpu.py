@@ -1,0 +1,186 @@
+"""GPU parity: the gfx950 kernels through the C ABI vs the oracle, bit for bit.
+
+Covers the reference's own vectors (KATs with every error variant, RFC 7541 App. C, the whole
+interop corpus), seeded random/error literals, edge cases (empty batch, empty literals, all-ones
+runs, unaligned blob base, tiny capacities) and, at the bench's full size, size-independent
+properties (encode -> decode round trip == input, per-literal lengths)."""
+
+import numpy as np
+import pytest
+
+from hpk_util import compare_batches, interop_literals, load, oracle_decode_batch, oracle_encode_batch, pack
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def codec():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a GPU (run with -m 'not gpu' on CPU)")
+    from loona_amd import HuffmanCodec
+
+    c = HuffmanCodec(0, stream=torch.cuda.current_stream())
+    yield c
+    c.close()
+
+
+def to_dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def gpu_decode(codec, blob, off, shift=0):
+    blob = np.ascontiguousarray(blob, np.uint8)
+    n = len(off) - 1
+    if shift:
+        pad = np.zeros(blob.size + shift + 1, np.uint8)
+        pad[shift : shift + blob.size] = blob
+        dblob = to_dev(pad)[shift:]
+    else:
+        dblob = to_dev(blob if blob.size else np.zeros(1, np.uint8))
+    doff = to_dev(np.asarray(off, np.int64).astype(np.int32))
+    out, oo, ol, st = codec.decode_device(dblob, doff, sync=True)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy(), oo.cpu().numpy().astype(np.uint32), ol[:n].cpu().numpy().astype(np.uint32),
+            st[:n].cpu().numpy())
+
+
+def gpu_encode(codec, blob, off):
+    n = len(off) - 1
+    dblob = to_dev(blob if blob.size else np.zeros(1, np.uint8))
+    doff = to_dev(np.asarray(off, np.int64).astype(np.int32))
+    out, oo, ol, st = codec.encode_device(dblob, doff, sync=True)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy(), oo.cpu().numpy().astype(np.uint32), ol[:n].cpu().numpy().astype(np.uint32),
+            st[:n].cpu().numpy())
+
+
+def test_kats_and_rfc(codec):
+    lits = [bytes.fromhex(k["in"]) for k in load("kat.json")]
+    lits += [bytes.fromhex(x["in"]) for x in load("rfc7541_blocks.json")["huffman_literals"]]
+    blob, off = pack(lits)
+    got = gpu_decode(codec, blob, off)
+    compare_batches(got, oracle_decode_batch(blob, off), "kat+rfc")
+    kats = load("kat.json")
+    for i, k in enumerate(kats):
+        assert got[3][i] == k["status"]
+
+
+def test_error_vectors(codec):
+    vecs = load("error_vectors.json")["vectors"]
+    lits = [bytes.fromhex(v["in"]) for v in vecs]
+    blob, off = pack(lits)
+    got = gpu_decode(codec, blob, off)
+    compare_batches(got, oracle_decode_batch(blob, off), "error vectors")
+    assert [int(s) for s in got[3]] == [v["status"] for v in vecs]
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_interop_corpus(codec, shift):
+    blob, off = pack(interop_literals())
+    compare_batches(gpu_decode(codec, blob, off, shift), oracle_decode_batch(blob, off), f"interop shift={shift}")
+
+
+def test_random_and_edge_literals(codec):
+    rng = np.random.default_rng(99)
+    lens = rng.integers(0, 70, size=50000)
+    lits = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+    lits += [b"", b"", b"\xff", b"\xff" * 3, b"\xff" * 4, b"\xff" * 5, b"\xff" * 40, b"\x00" * 9]
+    lits += [b""] * 70
+    blob, off = pack(lits)
+    compare_batches(gpu_decode(codec, blob, off), oracle_decode_batch(blob, off), "random")
+
+
+def test_empty_batch_and_empty_literals(codec):
+    blob, off = pack([])
+    got = gpu_decode(codec, blob, off)
+    assert got[2].size == 0
+    blob, off = pack([b""] * 1000)
+    got = gpu_decode(codec, blob, off)
+    assert not got[2].any() and not got[3].any()
+
+
+def test_host_pointer_mode(codec):
+    from loona_amd.batch import unpack
+
+    lits = interop_literals()[:5000]
+    blob, off = pack(lits)
+    out, oo, ol, st = codec.decode_host(blob, off)
+    compare_batches((out, oo, ol, st), oracle_decode_batch(blob, off), "host mode")
+    dec = unpack(out, oo, ol)
+    eb, eo = pack(dec)
+    e_out, e_oo, e_ol, e_st = codec.encode_host(eb, eo)
+    assert unpack(e_out, e_oo, e_ol) == lits
+
+
+def test_small_capacity_overflow(codec):
+    """Caller-provided capacity below the decoded size: status 4, no bytes past capacity."""
+    from loona_amd import huffman_encode
+
+    lits = [huffman_encode(b"abcdefghij" * k) for k in range(1, 30)]
+    blob, off = pack(lits)
+    n = len(lits)
+    cap = np.full(n, 7, np.int64)
+    oo = np.zeros(n + 1, np.int64)
+    np.cumsum(cap, out=oo[1:])
+    dblob, doff = to_dev(blob), to_dev(off.astype(np.int32))
+    doo = to_dev(oo.astype(np.int32))
+    out = torch.full((int(oo[-1]) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    codec.decode_into(dblob, doff, out, doo, ol, st, device=True, sync=True)
+    assert (st.cpu().numpy() == 4).all() and (ol.cpu().numpy() == 7).all()
+    assert (out[int(oo[-1]) :].cpu().numpy() == 0xAB).all()
+
+
+def test_encode_matches_oracle(codec):
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 200, size=20000)
+    strs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+    blob, off = pack(strs)
+    compare_batches(gpu_encode(codec, blob, off), oracle_encode_batch(blob, off), "encode")
+
+
+def test_config2_full_roundtrip(codec):
+    """BASELINE config 2 at full size (1M literals): GPU decode of the canonical encoding gives back
+    the generated strings exactly (size-independent property); a 100k prefix is also compared to
+    the oracle byte for byte."""
+    from loona_amd import synth
+
+    w = synth.config2()
+    got = gpu_decode(codec, w.enc_blob, w.enc_off)
+    out, oo, ol, st = got
+    assert not st.any()
+    assert np.array_equal(ol.astype(np.int64), np.diff(w.dec_off.astype(np.int64)))
+    ln = ol.astype(np.int64)
+    idx = np.repeat(oo[:-1].astype(np.int64) - (np.cumsum(ln) - ln), ln) + np.arange(int(ln.sum()))
+    assert np.array_equal(out[idx], w.dec_blob)
+    k = 100_000
+    sub_off = w.enc_off[: k + 1]
+    sub_blob = w.enc_blob[: int(sub_off[-1])]
+    compare_batches(gpu_decode(codec, sub_blob, sub_off), oracle_decode_batch(sub_blob, sub_off), "config2 prefix")
+
+
+def test_config3_roundtrip_sample(codec):
+    """BASELINE config 3 distribution (Zipf lengths to 4 KiB, 5 % uniform bytes): device encode ->
+    device decode == input; device encode == oracle encode on a 20k sample."""
+    from loona_amd import synth
+
+    w = synth.config3(n=20000)
+    e = gpu_encode(codec, w.dec_blob, w.dec_off)
+    compare_batches(e, oracle_encode_batch(w.dec_blob, w.dec_off), "config3 encode")
+    eo, eoo, eol, est = e
+    ln = eol.astype(np.int64)
+    idx = np.repeat(eoo[:-1].astype(np.int64) - (np.cumsum(ln) - ln), ln) + np.arange(int(ln.sum()))
+    enc_blob = eo[idx]
+    enc_off = np.zeros(len(ln) + 1, np.int64)
+    np.cumsum(ln, out=enc_off[1:])
+    d = gpu_decode(codec, enc_blob, enc_off.astype(np.uint32))
+    assert not d[3].any()
+    dl = d[2].astype(np.int64)
+    idx = np.repeat(d[1][:-1].astype(np.int64) - (np.cumsum(dl) - dl), dl) + np.arange(int(dl.sum()))
+    assert np.array_equal(d[0][idx], w.dec_blob)
