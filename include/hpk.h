@@ -77,7 +77,10 @@ typedef struct hpk_ctx hpk_ctx;
 
 hpk_ctx* hpk_ctx_create(int device);           /* NULL on failure (see hpk_last_error(NULL)) */
 void hpk_ctx_destroy(hpk_ctx* ctx);
-int hpk_ctx_set_stream(hpk_ctx* ctx, void* hip_stream); /* NULL = the ctx's own stream */
+/* Run on `hip_stream`: NULL = the ctx's own (non-blocking) stream; HPK_STREAM_LEGACY = the
+ * legacy null stream (stream 0, what torch's default stream is). */
+#define HPK_STREAM_LEGACY ((void*)(intptr_t)-1)
+int hpk_ctx_set_stream(hpk_ctx* ctx, void* hip_stream);
 void* hpk_ctx_stream(hpk_ctx* ctx);
 int hpk_ctx_sync(hpk_ctx* ctx);
 const char* hpk_last_error(const hpk_ctx* ctx); /* thread-local text of the last failure */

@@ -40,10 +40,16 @@ def unpack(blob, off, lens=None):
     return [blob[off[i] : off[i] + lens[i]].tobytes() for i in range(len(off) - 1)]
 
 
+def _round4(b):
+    return (b + 3) & ~3
+
+
 def decode_offsets_np(in_off):
-    """Output offsets from hpk_decoded_bound(len) = floor(8*len/5) per literal."""
+    """Output offsets from hpk_decoded_bound(len) = floor(8*len/5) per literal, each capacity
+    rounded up to 4 bytes so every literal's output starts dword-aligned (the kernels' fast
+    store path; unaligned offsets are still handled)."""
     in_off = np.asarray(in_off, dtype=np.int64)
-    b = (np.diff(in_off) * 8) // 5
+    b = _round4((np.diff(in_off) * 8) // 5)
     out = np.zeros(len(in_off), dtype=np.int64)
     np.cumsum(b, out=out[1:])
     if out[-1] >= 2**32:
@@ -52,9 +58,9 @@ def decode_offsets_np(in_off):
 
 
 def encode_offsets_np(in_off):
-    """Output offsets from hpk_encoded_bound(len) = ceil(30*len/8) per literal."""
+    """Output offsets from hpk_encoded_bound(len) = ceil(30*len/8) per literal (rounded to 4)."""
     in_off = np.asarray(in_off, dtype=np.int64)
-    b = (np.diff(in_off) * 30 + 7) // 8
+    b = _round4((np.diff(in_off) * 30 + 7) // 8)
     out = np.zeros(len(in_off), dtype=np.int64)
     np.cumsum(b, out=out[1:])
     if out[-1] >= 2**32:
@@ -104,9 +110,14 @@ class HuffmanCodec:
         self.close()
 
     def set_stream(self, stream):
-        """stream: a torch.cuda.Stream, a raw hipStream_t int, or None (the ctx's own)."""
-        raw = None if stream is None else int(getattr(stream, "cuda_stream", stream))
-        _lib.check(self._L.hpk_ctx_set_stream(self._h, ctypes.c_void_p(raw) if raw else None), "hpk_ctx_set_stream")
+        """stream: a torch.cuda.Stream (its handle 0 = the legacy null stream), a raw hipStream_t
+        int, or None (the ctx's own non-blocking stream)."""
+        if stream is None:
+            arg = None
+        else:
+            raw = int(getattr(stream, "cuda_stream", stream))
+            arg = ctypes.c_void_p(raw) if raw else ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)  # HPK_STREAM_LEGACY
+        _lib.check(self._L.hpk_ctx_set_stream(self._h, arg), "hpk_ctx_set_stream")
 
     def sync(self):
         _lib.check(self._L.hpk_ctx_sync(self._h), "hpk_ctx_sync")
@@ -196,7 +207,7 @@ def _bound_offsets_torch(in_off, num, den, add):
     import torch
 
     o = in_off.to(torch.int64)
-    b = ((o[1:] - o[:-1]) * num + add) // den
+    b = (((o[1:] - o[:-1]) * num + add) // den + 3) & ~3
     out = torch.zeros_like(o)
     torch.cumsum(b, 0, out=out[1:])
     if int(out[-1].item()) >= 2**32:

@@ -1,0 +1,165 @@
+// hpk_ctx.hip — device context and the batch entry points of the C ABI (include/hpk.h).
+#include <stdio.h>
+#include <string.h>
+
+#include "hpk_device.h"
+
+#define HPK_VERSION "hpk 0.2.1 gfx950 decode v2.1 (LDS window, lane queue, prefetch)"
+
+static thread_local std::string t_last_error;
+
+int hpk_set_err(const char* what, hipError_t e) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    t_last_error = buf;
+    return HPK_E_DEVICE;
+}
+
+int hpk_set_err_msg(const char* what, int code) {
+    t_last_error = what;
+    return code;
+}
+
+
+extern "C" const char* hpk_version(void) { return HPK_VERSION; }
+
+extern "C" const char* hpk_last_error(const hpk_ctx*) { return t_last_error.c_str(); }
+
+extern "C" hpk_ctx* hpk_ctx_create(int device) {
+    const hpk_tables* t = hpk_get_tables();
+    if (!t) { hpk_set_err_msg("code table build failed", HPK_E_INVAL); return nullptr; }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) { hpk_set_err("hipGetDeviceCount", e); return nullptr; }
+    if (device < 0 || device >= ndev) { hpk_set_err_msg("device index out of range", HPK_E_INVAL); return nullptr; }
+    hpk_ctx* c = new hpk_ctx();
+    c->device = device;
+    auto fail = [&](const char* what, hipError_t err) {
+        hpk_set_err(what, err);
+        hpk_ctx_destroy(c);
+        return (hpk_ctx*)nullptr;
+    };
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail("hipGetDeviceProperties", e);
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        hpk_set_err_msg("libhpk kernels are built for gfx950 only", HPK_E_NODEVICE);
+        delete c;
+        return nullptr;
+    }
+    c->num_cu = prop.multiProcessorCount;
+    if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", e);
+    c->stream = c->own;
+    if ((e = hipMalloc(&c->d_lut, sizeof(t->lut))) != hipSuccess) return fail("hipMalloc lut", e);
+    if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
+    if ((e = hipMalloc(&c->d_codes, 2 * 257 * sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc codes", e);
+    uint32_t packed[2 * 257];
+    for (int s = 0; s < 257; ++s) {
+        packed[s] = t->code[s];
+        packed[257 + s] = t->len[s];
+    }
+    if ((e = hipMemcpy(c->d_lut, t->lut, sizeof(t->lut), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload lut", e);
+    if ((e = hipMemcpy(c->d_lo, t->lo, sizeof(t->lo), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload lo", e);
+    if ((e = hipMemcpy(c->d_codes, packed, sizeof(packed), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload codes", e);
+    return c;
+}
+
+extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_lut);
+    (void)hipFree(c->d_lo);
+    (void)hipFree(c->d_codes);
+    (void)hipFree(c->d_in);
+    (void)hipFree(c->d_out);
+    (void)hipFree(c->d_meta);
+    (void)hipFree(c->d_st);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+extern "C" int hpk_ctx_set_stream(hpk_ctx* c, void* s) {
+    if (!c) return HPK_E_INVAL;
+    if (s == HPK_STREAM_LEGACY)
+        c->stream = (hipStream_t)0;
+    else
+        c->stream = s ? (hipStream_t)s : c->own;
+    return HPK_E_OK;
+}
+
+extern "C" void* hpk_ctx_stream(hpk_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int hpk_ctx_sync(hpk_ctx* c) {
+    if (!c) return HPK_E_INVAL;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return HPK_E_OK;
+}
+
+static int grow(void** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HPK_E_OK;
+    size_t n = need + need / 4 + 4096;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc(p, n));
+    *cap = n;
+    return HPK_E_OK;
+}
+
+static int check_offsets(const uint32_t* off, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (off[i + 1] < off[i]) return hpk_set_err_msg("offsets must be non-decreasing", HPK_E_INVAL);
+    return HPK_E_OK;
+}
+
+typedef int (*launch_fn)(hpk_ctx*, const uint8_t*, const uint32_t*, uint32_t, uint8_t*, const uint32_t*,
+                         uint32_t*, uint8_t*);
+
+static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
+                     uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int flags) {
+    if (!c || !in_off || !out_off || (n && (!out_len || !status))) return hpk_set_err_msg("null argument", HPK_E_INVAL);
+    HIP_TRY(hipSetDevice(c->device));
+    if (flags & HPK_PTR_DEVICE) {
+        if (n == 0) return HPK_E_OK;
+        if (!in_blob || !out_blob) return hpk_set_err_msg("null blob", HPK_E_INVAL);
+        int rc = fn(c, in_blob, in_off, n, out_blob, out_off, out_len, status);
+        if (rc) return rc;
+        if (!(flags & HPK_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));
+        return HPK_E_OK;
+    }
+    // host pointers: validate, stage, run, copy back
+    if (check_offsets(in_off, n) || check_offsets(out_off, n)) return HPK_E_INVAL;
+    if (n == 0) return HPK_E_OK;
+    const size_t in_bytes = in_off[n], out_bytes = out_off[n];
+    if ((in_bytes && !in_blob) || (out_bytes && !out_blob)) return hpk_set_err_msg("null blob", HPK_E_INVAL);
+    int rc;
+    if ((rc = grow((void**)&c->d_in, &c->d_in_cap, in_bytes + 16))) return rc;
+    if ((rc = grow((void**)&c->d_out, &c->d_out_cap, out_bytes + 16))) return rc;
+    if ((rc = grow((void**)&c->d_meta, &c->d_meta_cap, (3 * (size_t)n + 2) * 4))) return rc;
+    if ((rc = grow((void**)&c->d_st, &c->d_st_cap, n))) return rc;
+    uint32_t* d_in_off = c->d_meta;
+    uint32_t* d_out_off = c->d_meta + (n + 1);
+    uint32_t* d_len = c->d_meta + 2 * ((size_t)n + 1);
+    if (in_bytes) HIP_TRY(hipMemcpyAsync(c->d_in, in_blob, in_bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_in_off, in_off, (n + 1) * 4ull, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_out_off, out_off, (n + 1) * 4ull, hipMemcpyHostToDevice, c->stream));
+    if ((rc = fn(c, c->d_in, d_in_off, n, c->d_out, d_out_off, d_len, c->d_st))) return rc;
+    if (out_bytes) HIP_TRY(hipMemcpyAsync(out_blob, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_len, d_len, n * 4ull, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(status, c->d_st, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return HPK_E_OK;
+}
+
+extern "C" int hpk_decode_batch(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
+                                uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len, uint8_t* status,
+                                int flags) {
+    return run_batch(hpk_launch_decode, c, in_blob, in_off, n, out_blob, out_off, out_len, status, flags);
+}
+
+extern "C" int hpk_encode_batch(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
+                                uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len, uint8_t* status,
+                                int flags) {
+    return run_batch(hpk_launch_encode, c, in_blob, in_off, n, out_blob, out_off, out_len, status, flags);
+}

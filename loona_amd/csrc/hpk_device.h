@@ -1,0 +1,48 @@
+// hpk_device.h — shared between the device translation units of libhpk (context, decode, encode).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/hpk.h"
+#include "hpk_code.h"
+#include "hpk_internal.h"
+
+struct hpk_ctx {
+    int device = 0;
+    int num_cu = 256;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t* d_lut = nullptr;
+    uint16_t* d_lo = nullptr;
+    uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length
+    // grow-only scratch for HPK_PTR_HOST calls
+    uint8_t* d_in = nullptr;
+    size_t d_in_cap = 0;
+    uint8_t* d_out = nullptr;
+    size_t d_out_cap = 0;
+    uint32_t* d_meta = nullptr;  // in_off | out_off | out_len
+    size_t d_meta_cap = 0;
+    uint8_t* d_st = nullptr;
+    size_t d_st_cap = 0;
+};
+
+int hpk_set_err(const char* what, hipError_t e);
+int hpk_set_err_msg(const char* what, int code);
+
+#define HIP_TRY(call)                                            \
+    do {                                                         \
+        hipError_t _e = (call);                                  \
+        if (_e != hipSuccess) return hpk_set_err(#call, _e);     \
+    } while (0)
+
+// one-time per-process kernel attribute setup (dynamic LDS above 64 KiB)
+int hpk_decode_setup();
+
+int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
+                      const uint32_t* out_off, uint32_t* out_len, uint8_t* status);
+int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
+                      const uint32_t* out_off, uint32_t* out_len, uint8_t* status);
+
+__device__ __forceinline__ uint32_t hpk_bswap32(uint32_t x) { return __builtin_bswap32(x); }

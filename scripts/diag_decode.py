@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Diagnostics for the decode kernel (not part of the product): time one kernel variant
+(HPK_DEBUG_MODE env) on the config-2 batch and, in mode 3, dump per-wave timestamps."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from loona_amd import HuffmanCodec, _lib, synth  # noqa: E402
+from loona_amd.batch import decode_offsets_torch  # noqa: E402
+
+mode = int(os.environ.get("HPK_DEBUG_MODE", "0"))
+n = int(os.environ.get("DIAG_N", "1000000"))
+w = synth.config2(n=n)
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    codec = HuffmanCodec(0, stream=s)
+    blob = torch.from_numpy(w.enc_blob).cuda()
+    io = torch.from_numpy(w.enc_off.astype(np.int32)).cuda()
+    oo = decode_offsets_torch(io)
+    out = torch.empty(int(oo[-1].item()) + 16, dtype=torch.uint8, device="cuda")
+    ol = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for _ in range(5):
+        codec.decode_into(blob, io, out, oo, ol, st)
+    s.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    K = 20
+    for _ in range(K):
+        codec.decode_into(blob, io, out, oo, ol, st)
+    e1.record(s)
+    s.synchronize()
+    us = e0.elapsed_time(e1) / K * 1e3
+res = {"mode": mode, "us_per_launch": round(us, 2)}
+if mode in (0, 2, 3, 4):
+    ok = bool((st.cpu().numpy() == 0).all()) and np.array_equal(ol.cpu().numpy(), np.diff(w.dec_off.astype(np.int64)))
+    res["lengths_ok"] = ok
+if mode == 4:
+    L = _lib.lib()
+    L.hpk_debug_check.argtypes = [ctypes.c_void_p]
+    chk = np.zeros(8, np.uint64)
+    L.hpk_debug_check(chk.ctypes.data)
+    res["check"] = [int(x) for x in chk]
+if mode == 3:
+    L = _lib.lib()
+    L.hpk_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    buf = np.zeros(256 * 16 * 4, np.uint64)
+    got = L.hpk_debug_stamps(buf.ctypes.data, buf.size)
+    st4 = buf[:got].reshape(-1, 4).astype(np.int64)
+    t0 = st4[:, 0].min()
+    start = (st4[:, 0] - t0) / 100.0  # s_memtime ticks at shader clock? report raw ticks too
+    staged = (st4[:, 1] - st4[:, 0])
+    total = (st4[:, 2] - st4[:, 0])
+    res["stamp_ticks"] = {
+        "start_spread": int(st4[:, 0].max() - t0),
+        "stage_med": int(np.median(staged)), "stage_max": int(staged.max()),
+        "total_med": int(np.median(total)), "total_p90": int(np.percentile(total, 90)), "total_max": int(total.max()),
+        "end_spread": int(st4[:, 2].max() - t0),
+        "xcc_counts": np.bincount((st4[:, 3] >> 32).astype(np.int64), minlength=8).tolist(),
+    }
+print(json.dumps(res), flush=True)
