@@ -1,0 +1,143 @@
+// kvariants.hip — development harness (not part of the product): times decode-kernel variants
+// (refill period, ILP) on one batch in a single process and checks each against the library's
+// CPU path (hpk_decode_batch_cpu, itself pinned to the oracle by tests/test_host.py).
+// Input file (written by scripts/kinput.py): u32 n, u32 enc_bytes, u32 in_off[n+1], u8 blob[].
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../loona_amd/csrc/hpk_decode_kernel.h"
+
+using namespace hpkdec;
+
+int hpk_set_err(const char*, hipError_t) { return -3; }
+int hpk_set_err_msg(const char*, int c) { return c; }
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(2);                                                               \
+        }                                                                          \
+    } while (0)
+
+struct Dev {
+    DecodeArgs a;
+    uint32_t n;
+    size_t out_bytes;
+};
+
+template <int kMode, int kW, int kD, int kM, int kR, int kC, int kBlocksPerCu = 1>
+static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
+                const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
+    using G = BlockGeometry<kW, kD, kM>;
+    auto fn = hpk_decode_kernel<kMode, kW, kD, kM, kR, kC>;
+    const int kLdsBytes = G::kLdsBytes;
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+    dim3 grid(num_cu * kBlocksPerCu), block(G::kBlock);
+    CK(hipMemset(d.a.out_len, 0xFF, d.n * 4));
+    CK(hipMemset(d.a.out_base, 0xAB, d.out_bytes));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, grid, block, kLdsBytes, 0, d.a);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(fn, grid, block, kLdsBytes, 0, d.a);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<uint32_t> len(d.n);
+    std::vector<uint8_t> st(d.n), out(d.out_bytes);
+    CK(hipMemcpy(len.data(), d.a.out_len, d.n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(st.data(), d.a.status, d.n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(out.data(), d.a.out_base, d.out_bytes, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (uint32_t i = 0; i < d.n; ++i)
+        if (len[i] != ref_len[i] || st[i] != ref_st[i]) ++bad;
+    // compare valid bytes
+    std::vector<uint32_t> oo(d.n + 1);
+    CK(hipMemcpy(oo.data(), d.a.out_off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
+    size_t badb = 0;
+    if (kMode == 0)
+        for (uint32_t i = 0; i < d.n; ++i)
+            if (memcmp(&out[oo[i]], &ref_out[oo[i]], ref_len[i]) != 0) ++badb;
+    printf("{\"variant\": \"%s\", \"us\": %.2f, \"bad_len_status\": %zu, \"bad_bytes\": %zu}\n", name,
+           ms * 1000.0 / iters, bad, badb);
+    fflush(stdout);
+}
+
+extern "C" int hpk_decode_batch_cpu(const uint8_t*, const uint32_t*, uint32_t, uint8_t*, const uint32_t*, uint32_t*,
+                                    uint8_t*, int);
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 1;
+    FILE* f = fopen(argv[1], "rb");
+    uint32_t n, eb;
+    if (fread(&n, 4, 1, f) != 1 || fread(&eb, 4, 1, f) != 1) return 1;
+    std::vector<uint32_t> in_off(n + 1);
+    std::vector<uint8_t> blob(eb + 16);
+    if (fread(in_off.data(), 4, n + 1, f) != n + 1 || fread(blob.data(), 1, eb, f) != eb) return 1;
+    fclose(f);
+    const int iters = argc > 2 ? atoi(argv[2]) : 20;
+    std::vector<uint32_t> out_off(n + 1);
+    out_off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) out_off[i + 1] = out_off[i] + ((((in_off[i + 1] - in_off[i]) * 8) / 5 + 3) & ~3u);
+    const size_t ob = out_off[n] + 16;
+    std::vector<uint8_t> ref_out(ob);
+    std::vector<uint32_t> ref_len(n);
+    std::vector<uint8_t> ref_st(n);
+    hpk_decode_batch_cpu(blob.data(), in_off.data(), n, ref_out.data(), out_off.data(), ref_len.data(), ref_st.data(), 0);
+
+    hpk_tables tab;
+    hpk_build_tables(&tab);
+    Dev d;
+    d.n = n;
+    d.out_bytes = ob;
+    uint8_t *d_in, *d_out, *d_st;
+    uint32_t *d_io, *d_oo, *d_len, *d_lut;
+    uint16_t* d_lo;
+    CK(hipMalloc(&d_in, eb + 64));
+    CK(hipMalloc(&d_out, ob));
+    CK(hipMalloc(&d_st, n));
+    CK(hipMalloc(&d_io, (n + 1) * 4));
+    CK(hipMalloc(&d_oo, (n + 1) * 4));
+    CK(hipMalloc(&d_len, n * 4));
+    CK(hipMalloc(&d_lut, sizeof(tab.t8)));
+    CK(hipMalloc(&d_lo, sizeof(tab.lo)));
+    CK(hipMemcpy(d_in, blob.data(), eb, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_io, in_off.data(), (n + 1) * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_oo, out_off.data(), (n + 1) * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_lut, tab.t8, sizeof(tab.t8), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_lo, tab.lo, sizeof(tab.lo), hipMemcpyHostToDevice));
+    DecodeArgs& a = d.a;
+    a.in_base = d_in;
+    a.in_mis = 0;
+    a.in_off = d_io;
+    a.n = n;
+    a.out_base = d_out;
+    a.out_mis = 0;
+    a.out_off = d_oo;
+    a.out_len = d_len;
+    a.status = d_st;
+    a.t8 = reinterpret_cast<const uint8_t*>(d_lut);
+    a.lo = d_lo;
+    a.dbg = nullptr;
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cu = prop.multiProcessorCount;
+    printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
+    run<0, 16, 126976, 4096, 4, 64>("b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 3, 64>("b16_r3_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 6, 64>("b16_r6_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 4, 32>("b16_r4_c32", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 4, 128>("b16_r4_c128", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 4, 256>("b16_r4_c256", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 8, 61440, 2048, 4, 64, 2>("b8x2_r4_c64_2pc", d, ref_len, ref_st, ref_out, cu, iters);
+    run<2, 16, 126976, 4096, 4, 64>("nostore_b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    return 0;
+}

@@ -7,7 +7,7 @@
 // them on every literal (huffman.rs:58-82, decoder.rs:148). Here the tables are built once per
 // context and staged in LDS by the kernels.
 //
-// Two decode tables (both validated by tests/test_tables.py and the golden vectors):
+// Decode tables (built and self-checked below; validated end to end by the golden vectors):
 //
 //  * LUT  (HPK_LUT_BITS-bit index = the next bits of the stream, MSB-first). Entry (u32):
 //        [7:0] sym0  [15:8] sym1  [20:16] len0  [25:21] len0+len1  [27:26] nsym (0,1,2)
@@ -25,6 +25,15 @@
 #define HPK_LUT_SIZE (1u << HPK_LUT_BITS)
 #define HPK_LO_RUNS 30
 #define HPK_LO_SIZE (HPK_LO_RUNS * 32)
+
+// Canonical limits of the 5..8-bit codes (left-aligned 32-bit window): a window below LIM5 starts
+// with a 5-bit code, below LIM6 a 6-bit one, below LIM7 7, below LIM8 8; at or above LIM8 the
+// code is 10..30 bits long. These four lengths cover ~99.9 % of header-value symbols, so the
+// decoder computes the length arithmetically and reads only the symbol from a table (T8).
+#define HPK_LIM5 0x50000000u
+#define HPK_LIM6 0xB8000000u
+#define HPK_LIM7 0xF8000000u
+#define HPK_LIM8 0xFE000000u
 
 // Code length of every symbol 0..255 and EOS (256). RFC 7541 Appendix B, column "len in bits".
 static const uint8_t HPK_CODE_LEN[HPK_NSYM] = {
@@ -52,6 +61,7 @@ struct hpk_tables {
     uint8_t len[HPK_NSYM];     // code length in bits
     uint32_t lut[HPK_LUT_SIZE];
     uint16_t lo[HPK_LO_SIZE];
+    uint8_t t8[256];  // symbol of the <=8-bit code that prefixes each 8-bit window (0 past LIM8)
 };
 
 // Build canonical codes from lengths, then the LUT and LO tables. Returns 0 on success,
@@ -90,6 +100,19 @@ static inline int hpk_build_tables(hpk_tables* t) {
             if (e == 0xFFFF) return -1;
             t->lo[k * 32 + t5] = e;
         }
+
+    // T8: the symbol whose (<= 8-bit) code prefixes each 8-bit window; check the limits too.
+    for (uint32_t v = 0; v < 256; ++v) {
+        t->t8[v] = 0;
+        const uint32_t w = v << 24;
+        if (w >= HPK_LIM8) continue;
+        const int L = 5 + (w >= HPK_LIM5) + (w >= HPK_LIM6) + (w >= HPK_LIM7);
+        int found = -1;
+        for (int s = 0; s < 256; ++s)
+            if (t->len[s] <= 8 && (w >> (32 - t->len[s])) == t->code[s]) { found = s; break; }
+        if (found < 0 || t->len[found] != L) return -1;
+        t->t8[v] = (uint8_t)found;
+    }
 
     // LUT: up to two whole codes inside the first HPK_LUT_BITS bits.
     for (uint32_t v = 0; v < HPK_LUT_SIZE; ++v) {

@@ -4,7 +4,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.2.1 gfx950 decode v2.1 (LDS window, lane queue, prefetch)"
+#define HPK_VERSION "hpk 0.5 gfx950 decode v5 (block LDS window, block queue, arithmetic code lengths)"
 
 static thread_local std::string t_last_error;
 
@@ -52,6 +52,8 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     c->stream = c->own;
     if ((e = hipMalloc(&c->d_lut, sizeof(t->lut))) != hipSuccess) return fail("hipMalloc lut", e);
     if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
+    if ((e = hipMalloc(&c->d_t8, sizeof(t->t8))) != hipSuccess) return fail("hipMalloc t8", e);
+    if ((e = hipMemcpy(c->d_t8, t->t8, sizeof(t->t8), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload t8", e);
     if ((e = hipMalloc(&c->d_codes, 2 * 257 * sizeof(uint32_t))) != hipSuccess) return fail("hipMalloc codes", e);
     uint32_t packed[2 * 257];
     for (int s = 0; s < 257; ++s) {
@@ -70,6 +72,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->d_lut);
     (void)hipFree(c->d_lo);
+    (void)hipFree(c->d_t8);
     (void)hipFree(c->d_codes);
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);

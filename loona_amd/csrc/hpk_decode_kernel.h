@@ -1,0 +1,453 @@
+// hpk_decode_kernel.h — the gfx950 decode kernel template (design notes in hpk_decode.hip).
+// Shared by the library (hpk_decode.hip) and the variant harness (bench/kvariants.hip).
+#pragma once
+#include <stdint.h>
+
+#include "hpk_device.h"
+
+namespace hpkdec {
+
+// Tables in LDS (once per workgroup): T8 (256 B, symbols of the <= 8-bit codes) and the
+// leading-ones table LO (1.9 KiB, any code). 16-byte aligned carve-outs.
+constexpr int kT8Bytes = 256;
+constexpr int kLoBytes = HPK_LO_SIZE * 2;
+constexpr int kTabBytes = ((kT8Bytes + kLoBytes + 15) / 16) * 16;
+
+struct DecodeArgs {
+    const uint8_t* in_base;  // in_blob rounded down to 16 bytes
+    uint32_t in_mis;         // in_blob - in_base (0..15)
+    const uint32_t* in_off;
+    uint32_t n;
+    uint8_t* out_base;  // out_blob rounded down to 4 bytes
+    uint32_t out_mis;   // out_blob - out_base (0..3)
+    const uint32_t* out_off;
+    uint32_t* out_len;
+    uint8_t* status;
+    const uint8_t* t8;
+    const uint16_t* lo;
+    unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
+};
+
+// Per-lane state of the literal being decoded.
+struct Lit {
+    uint64_t win;   // next bits, MSB-aligned (bits past the literal: whatever follows)
+    uint32_t nb;    // loaded bits in win
+    uint32_t nxt;   // next source dword (raw), merged at the next refill
+    uint32_t pf;    // the dword after it (raw, read one refill ahead)
+    uint32_t q;     // source dword index of pf
+    uint32_t rem;   // literal bits not yet consumed
+    uint32_t cnt;   // bytes decoded
+    uint32_t st;    // hpk_status
+    uint64_t acc;   // pending output bytes (little-endian order)
+    uint32_t accn;  // bytes in acc
+    uint32_t od;    // output dword index (dword stores) or byte position (byte stores)
+    uint32_t ocap;  // output capacity (byte stores only)
+    uint32_t oend;  // diagnostic mode 4: one past the last output dword of the literal
+    bool live;      // still decoding
+};
+
+enum StoreMode { kDword = 0, kNoStore = 1, kChecked = 3 };
+
+// diagnostic mode 4: record the first out-of-region store instead of performing it
+__device__ unsigned long long g_chk[8];
+__device__ __forceinline__ void chk_report(uint32_t code, uint32_t a0, uint32_t a1, uint32_t a2) {
+    if (atomicCAS(&g_chk[0], 0ull, (unsigned long long)code) == 0ull) {
+        g_chk[1] = a0;
+        g_chk[2] = a1;
+        g_chk[3] = a2;
+        g_chk[4] = blockIdx.x;
+        g_chk[5] = threadIdx.x;
+    }
+}
+
+template <class Src>
+__device__ __forceinline__ void lit_begin(Lit& L, const Src& src, uint32_t sb, uint32_t nbytes) {
+    L.rem = nbytes * 8u;
+    L.cnt = 0;
+    L.st = HPK_OK;
+    L.live = nbytes != 0;
+    L.acc = 0;
+    L.accn = 0;
+    const uint32_t q0 = sb >> 2;
+    const uint32_t sk = (sb & 3u) * 8u;
+    const uint32_t d0 = src(q0);
+    L.nxt = src(q0 + 1);
+    L.pf = src(q0 + 2);
+    L.q = q0 + 2;
+    L.win = ((uint64_t)hpk_bswap32(d0) << 32) << sk;
+    L.nb = 32u - sk;
+}
+
+// Top the window up to >= 32 bits from the prefetched dword; read the next one.
+template <class Src>
+__device__ __forceinline__ void lit_refill(Lit& L, const Src& src) {
+    const bool need = L.nb <= 32u;
+    const uint64_t add = (uint64_t)hpk_bswap32(L.nxt) << ((32u - L.nb) & 63u);
+    L.win |= need ? add : 0ull;
+    L.nb += need ? 32u : 0u;
+    L.nxt = need ? L.pf : L.nxt;
+    L.q += need ? 1u : 0u;
+    L.pf = src(L.q);
+}
+
+// Decode one code of any length from the window (>= 30 loaded bits): leading-ones table.
+__device__ __forceinline__ void lo_decode(uint32_t w, const uint16_t* __restrict__ lo, uint32_t& sym,
+                                          uint32_t& len, bool& eos) {
+    const uint32_t kk = __clz(~w);
+    const uint32_t e = lo[min(kk, (uint32_t)HPK_LO_RUNS - 1) * 32 + ((w << ((kk + 1) & 31)) >> 27)];
+    eos = kk >= HPK_LO_RUNS || (e & 0x1FFu) == HPK_EOS;
+    sym = e & 0xFFu;
+    len = eos ? 30u : (e >> 9);
+}
+
+// Append g (<= 4) bytes to the pending output; store a whole dword when one is complete.
+template <int kStore>
+__device__ __forceinline__ void lit_emit(Lit& L, uint32_t packed, uint32_t g, uint8_t* __restrict__ out8) {
+    L.acc |= (uint64_t)packed << (8u * L.accn);
+    L.accn += g;
+    L.cnt += g;
+    if (L.accn >= 4u) {
+        if (kStore == kDword) {
+            reinterpret_cast<uint32_t*>(out8)[L.od] = (uint32_t)L.acc;
+        } else if (kStore == kChecked) {
+            if (L.od < L.oend)
+                reinterpret_cast<uint32_t*>(out8)[L.od] = (uint32_t)L.acc;
+            else
+                chk_report(1, L.od, L.oend, L.cnt);
+        } else {
+            asm volatile("" ::"v"((uint32_t)L.acc));
+        }
+        L.od += 1;
+        L.acc >>= 32;
+        L.accn -= 4u;
+    }
+}
+
+// One step: refill, then 4 codes decoded speculatively as if all were 5..8-bit codes: lengths
+// from the canonical limits (no memory access on the serial chain), symbols from T8 off that
+// chain, running bit offsets c1..c4. The valid prefix (fast code, ends inside the literal, lane
+// live) is then consumed and emitted with a handful of selects. The first invalid code either
+// runs past the literal's end (only padding left: the lane stops) or is a 10..30-bit code / EOS:
+// the lane "parks" and that one code is decoded with the leading-ones table (one branch per
+// step, taken only when some lane needs it).
+template <int kStore, class Src>
+__device__ __forceinline__ void lit_step(Lit& L, const Src& src, const uint8_t* __restrict__ t8,
+                                         const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8) {
+    lit_refill(L, src);  // >= 32 bits loaded: four 8-bit codes fit
+    uint64_t x = L.win;
+    uint32_t c[5], sym[4];
+    bool fast[4];
+    c[0] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w = (uint32_t)(x >> 32);
+        const uint32_t len = 5u + (w >= HPK_LIM5) + (w >= HPK_LIM6) + (w >= HPK_LIM7);
+        fast[i] = w < HPK_LIM8;
+        sym[i] = t8[w >> 24];
+        c[i + 1] = c[i] + len;
+        x <<= len;
+    }
+    // valid prefix: m_i = lane live and codes 0..i are fast and end inside the literal
+    const bool m0 = L.live && fast[0] && c[1] <= L.rem;
+    const bool m1 = m0 && fast[1] && c[2] <= L.rem;
+    const bool m2 = m1 && fast[2] && c[3] <= L.rem;
+    const bool m3 = m2 && fast[3] && c[4] <= L.rem;
+    const uint32_t use = m3 ? c[4] : m2 ? c[3] : m1 ? c[2] : m0 ? c[1] : 0u;
+    const uint32_t g = m3 ? 4u : m2 ? 3u : m1 ? 2u : m0 ? 1u : 0u;
+    // the first invalid code: a long code (park for the LO lookup) or the literal's end
+    const bool bad_fast = m2 ? fast[3] : m1 ? fast[2] : m0 ? fast[1] : fast[0];
+    const bool park = L.live && !m3 && !bad_fast;
+    L.win <<= use;
+    L.nb -= use;
+    L.rem -= use;
+    uint32_t packed = sym[0] | (sym[1] << 8) | (sym[2] << 16) | (sym[3] << 24);
+    packed &= g >= 4u ? 0xFFFFFFFFu : ((1u << (8u * g)) - 1u);
+    lit_emit<kStore>(L, packed, g, out8);
+    L.live = park || (m3 && L.rem != 0u);
+    if (park) {  // a 10..30-bit code (or EOS): one lookup in the leading-ones table
+        lit_refill(L, src);
+        const uint32_t w = (uint32_t)(L.win >> 32);
+        uint32_t s1, len;
+        bool eos;
+        lo_decode(w, lo, s1, len, eos);
+        if (len > L.rem) {
+            L.live = false;  // only padding left
+        } else if (eos) {
+            L.st = HPK_EOS_IN_STRING;  // huffman.rs:112-116
+            L.live = false;
+        } else {
+            L.win <<= len;
+            L.nb -= len;
+            L.rem -= len;
+            lit_emit<kStore>(L, s1, 1u, out8);
+            L.live = L.rem != 0u;
+        }
+    }
+}
+
+template <int kStore>
+__device__ __forceinline__ void lit_finish(Lit& L, const DecodeArgs& a, uint32_t i) {
+    // the last, partial dword lies inside this literal's capacity (aligned, >= decoded bound)
+    if (kStore == kDword && L.accn) reinterpret_cast<uint32_t*>(a.out_base)[L.od] = (uint32_t)L.acc;
+    if (kStore == kChecked && L.accn) {
+        if (L.od < L.oend)
+            reinterpret_cast<uint32_t*>(a.out_base)[L.od] = (uint32_t)L.acc;
+        else
+            chk_report(2, L.od, L.oend, L.cnt);
+    }
+    if (kStore == kChecked && i >= a.n) {
+        chk_report(3, i, a.n, 0);
+        return;
+    }
+    uint32_t st = L.st;
+    if (st == HPK_OK && L.rem > 0) {  // huffman.rs:128-160: at most 7 bits, all ones (EOS MSBs)
+        if (L.rem > 7) {
+            st = HPK_PADDING_TOO_LARGE;
+        } else {
+            const uint32_t w = (uint32_t)(L.win >> 32) | (0xFFFFFFFFu >> L.rem);
+            if (w != 0xFFFFFFFFu) st = HPK_INVALID_PADDING;
+        }
+    }
+    a.out_len[i] = L.cnt;
+    a.status[i] = (uint8_t)st;
+}
+
+// Literal i decoded whole, one code at a time, with byte stores and per-byte capacity checks:
+// output regions that are unaligned or below hpk_decoded_bound, and literals too long for the
+// LDS window (read from global memory).
+template <class Src>
+__device__ __forceinline__ void lit_bytes(const Src& src, const uint16_t* lo, const DecodeArgs& a, uint32_t i,
+                                          uint32_t sb, uint32_t nbytes) {
+    Lit L;
+    lit_begin(L, src, sb, nbytes);
+    uint32_t o = a.out_off[i] + a.out_mis;
+    const uint32_t ocap = a.out_off[i + 1] - a.out_off[i];
+    while (L.live) {
+        lit_refill(L, src);
+        uint32_t sym, len;
+        bool eos;
+        lo_decode((uint32_t)(L.win >> 32), lo, sym, len, eos);
+        if (len > L.rem) break;
+        if (eos) {
+            L.st = HPK_EOS_IN_STRING;
+            break;
+        }
+        if (L.cnt >= ocap) {
+            L.st = HPK_OUTPUT_OVERFLOW;
+            break;
+        }
+        a.out_base[o + L.cnt] = (uint8_t)sym;
+        L.cnt += 1;
+        L.win <<= len;
+        L.nb -= len;
+        L.rem -= len;
+        L.live = L.rem != 0u;
+    }
+    L.accn = 0;
+    lit_finish<kNoStore>(L, a, i);
+}
+
+struct LdsSrc {
+    const uint32_t* p;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
+};
+struct GlobalSrc {
+    const uint32_t* p;
+    uint32_t last;  // last dword index holding a byte of the batch: never read past it
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[min(i, last)]; }
+};
+
+// Block-level window (v5): the workgroup stages a contiguous run of its literals into one LDS
+// window shared by all its waves, and every wave pulls literals from ONE block queue (an LDS
+// counter). Waves of a SIMD are arbitrated by age, so with a static per-wave split the youngest
+// wave of each SIMD finished ~1.8x later than the oldest; with a shared queue fast waves simply
+// take more literals and all finish together.
+template <int kWaves, int kData, int kMaxLits>
+struct BlockGeometry {
+    static constexpr int kBlock = kWaves * 64;
+    static constexpr int kMetaRounds = (kMaxLits + kBlock - 1) / kBlock;
+    static constexpr int kStageRounds = (kData / 16 + kBlock - 1) / kBlock;
+    static constexpr int kQueueOff = kTabBytes + kData;
+    static constexpr int kCtrOff = kQueueOff + kMaxLits * 8;
+    static constexpr int kLdsBytes = kCtrOff + 16;
+    static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+    static_assert(kData % 16 == 0 && kData <= (1 << 17), "window offsets pack in 17 bits");
+};
+constexpr uint32_t kQByte = 0x80000000u;  // queue entry .y flag: byte path
+
+// kMode: 0 = product kernel; diagnostic variants (HPK_DEBUG_MODE, never the default):
+//   1 = stage only (no decode), 2 = decode without output stores, 3 = product + per-wave stamps,
+//   4 = every global store bounds-checked (first violation recorded in g_chk, store skipped)
+template <int kMode, int kWaves, int kData, int kMaxLits, int kRefillN, int kChunk>
+__global__ __launch_bounds__(kWaves * 64) void hpk_decode_kernel(DecodeArgs a) {
+    using G = BlockGeometry<kWaves, kData, kMaxLits>;
+    unsigned long long t_start = 0, t_staged = 0;
+    if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* s_t8 = smem;
+    uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
+    uint8_t* s_data = smem + kTabBytes;
+    uint2* s_q = reinterpret_cast<uint2*>(smem + G::kQueueOff);
+    uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);  // [0] fitting count, [1] queue head
+    for (uint32_t t = threadIdx.x; t < kT8Bytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_t8)[t] = reinterpret_cast<const uint4*>(a.t8)[t];
+    for (uint32_t t = threadIdx.x; t < kLoBytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const LdsSrc lds{reinterpret_cast<const uint32_t*>(s_data)};
+    const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
+    const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+
+    uint32_t cur = BA;
+    while (cur < BB) {  // block-uniform
+        const uint32_t cntl = min((uint32_t)kMaxLits, BB - cur);
+        const uint32_t base16 = (a.in_off[cur] + a.in_mis) & ~15u;
+        const uint32_t limit = base16 + kData;
+        __syncthreads();  // previous fill fully drained (queue, window and counters free)
+        if (tid == 0) {
+            s_ctr[0] = 0;
+            s_ctr[1] = G::kBlock;
+        }
+        __syncthreads();
+        // offsets: all loads issued first (clamped indices), then used
+        uint32_t io0[G::kMetaRounds], io1[G::kMetaRounds], oo0[G::kMetaRounds], oo1[G::kMetaRounds];
+#pragma unroll
+        for (int r = 0; r < G::kMetaRounds; ++r) {
+            const uint32_t t = min(tid + (uint32_t)G::kBlock * r, cntl - 1);
+            io0[r] = a.in_off[cur + t];
+            io1[r] = a.in_off[cur + t + 1];
+            oo0[r] = a.out_off[cur + t];
+            oo1[r] = a.out_off[cur + t + 1];
+        }
+        uint32_t kw = 0;
+#pragma unroll
+        for (int r = 0; r < G::kMetaRounds; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            const uint32_t p0 = io0[r] + a.in_mis, p1 = io1[r] + a.in_mis;
+            const bool fits = t < cntl && p1 <= limit;
+            if (fits) {
+                const uint32_t nbytes = p1 - p0;
+                const uint32_t o = oo0[r] + a.out_mis, ocap = oo1[r] - oo0[r];
+                // dword path needs an aligned region holding hpk_decoded_bound(nbytes) bytes (and a
+                // length that packs in 15 bits); byte-path entries carry the length in .y instead
+                const bool dw = ((o | ocap) & 3u) == 0 && ocap >= (nbytes * 8u) / 5u && nbytes < 32768u;
+                s_q[t] = dw ? make_uint2((p0 - base16) | (nbytes << 17), o >> 2)
+                            : make_uint2(p0 - base16, kQByte | nbytes);
+            }
+            kw += (uint32_t)__popcll(__ballot(fits));
+        }
+        if (lane == 0 && kw) atomicAdd(&s_ctr[0], kw);
+        __syncthreads();
+        const uint32_t k = s_ctr[0];
+        if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global
+            if (tid == 0) {
+                const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), (a.in_off[a.n] + a.in_mis - 1) >> 2};
+                const uint32_t sb = a.in_off[cur] + a.in_mis;
+                lit_bytes(g, s_lo, a, cur, sb, a.in_off[cur + 1] + a.in_mis - sb);
+            }
+            cur += 1;
+            continue;
+        }
+        // stage the window's bytes with 16-byte loads: all loads issued, then all LDS writes.
+        // Chunks are 16-byte aligned and each holds a byte of the batch, so no page is crossed.
+        const uint2 last = s_q[k - 1];
+        const uint32_t endb = (last.x & 0x1FFFFu) + ((last.y & kQByte) ? (last.y & ~kQByte) : (last.x >> 17));
+        uint32_t nch = (endb + 15) >> 4;
+        if (kMode == 4 && (nch > kData / 16 || base16 + endb > a.in_off[a.n] + a.in_mis + 16)) {
+            chk_report(5, nch, endb, base16);
+            nch = 0;
+        }
+        if (nch) {
+            const uint4* g16 = reinterpret_cast<const uint4*>(a.in_base + base16);
+            uint4* l16 = reinterpret_cast<uint4*>(s_data);
+            uint4 chunk[G::kStageRounds];
+#pragma unroll
+            for (int r = 0; r < G::kStageRounds; ++r) chunk[r] = g16[min(tid + (uint32_t)G::kBlock * r, nch - 1)];
+#pragma unroll
+            for (int r = 0; r < G::kStageRounds; ++r)
+                if (tid + (uint32_t)G::kBlock * r < nch) l16[tid + G::kBlock * r] = chunk[r];
+        }
+        __syncthreads();
+        if (kMode == 3 && t_staged == 0) t_staged = __builtin_amdgcn_s_memtime();
+        if (kMode == 1) {  // diagnostic: keep the staged bytes live, write lengths only
+            for (uint32_t t = tid; t < k; t += G::kBlock) {
+                const uint2 e = s_q[t];
+                a.out_len[cur + t] = e.x + s_data[e.x & 0x1FFFFu];
+                a.status[cur + t] = 0;
+            }
+        } else {
+            // decode [0, k) from the block queue
+            constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
+            Lit L = {};  // every field defined: idle lanes still run the (predicated) step
+            L.nb = 64;
+            uint32_t t = tid;
+            uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
+            bool act = false;         // lane holds a dword-path literal not yet finalised
+            // Branch-free (re)start: lanes past the queue read a clamped entry and stay idle. Keeping
+            // the loop free of divergent exits matters: the ballots below must see the whole wave.
+            auto begin = [&](uint32_t tt) {
+                const uint2 e = s_q[min(tt, k - 1)];
+                act = tt < k && !(e.y & kQByte);
+                lit_begin(L, lds, e.x & 0x1FFFFu, e.x >> 17);
+                L.od = e.y;
+                L.oend = e.y + ((e.x >> 17) * 8u / 5u + 3u) / 4u;
+                L.live = L.live && act;
+            };
+            begin(t);
+            for (;;) {
+#pragma unroll
+                for (int s = 0; s < kRefillN; ++s) lit_step<kStore>(L, lds, s_t8, s_lo, a.out_base);
+                const bool fin = t < k && !L.live;
+                if (__any(fin)) {
+                    if (fin && act) lit_finish<kStore>(L, a, cur + t);
+                    const bool free_lane = fin || t >= k;
+                    const uint64_t fm = __ballot(free_lane);
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+                    // free lanes take the wave's reserved slots [qb, qe) in rank order; when those
+                    // run short the wave reserves kChunk more with one LDS atomic (block queue)
+                    const uint32_t need = (uint32_t)__popcll(fm), have = qe - qb;
+                    uint32_t base = qb + rank;
+                    if (have < need) {  // wave-uniform
+                        uint32_t nb = 0;
+                        if (rank == 0 && free_lane) nb = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
+                        nb = (uint32_t)__builtin_amdgcn_readlane((int)nb, (int)__builtin_ctzll(fm));
+                        if (rank >= have) base = nb + (rank - have);
+                        qb = nb + (need - have);
+                        qe = nb + kChunk;
+                    } else {
+                        qb += need;
+                    }
+                    qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
+                    qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
+                    const uint32_t tn = free_lane ? base : t;
+                    if (free_lane) {
+                        t = tn;
+                        begin(tn);
+                    }
+                }
+                if (!__any(t < k)) break;
+            }
+            // literals whose output region is unaligned / below the decoded bound
+            for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
+                const uint2 e = s_q[tt];
+                if (e.y & kQByte) lit_bytes(lds, s_lo, a, cur + tt, e.x & 0x1FFFFu, e.y & ~kQByte);
+            }
+        }
+        cur += k;
+    }
+    if (kMode == 3 && lane == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        const uint64_t gwi = (uint64_t)blockIdx.x * kWaves + (tid >> 6);
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.dbg[gwi * 4 + 0] = t_start;
+        a.dbg[gwi * 4 + 1] = t_staged;
+        a.dbg[gwi * 4 + 2] = t_end;
+        a.dbg[gwi * 4 + 3] = ((unsigned long long)xcc << 32) | (BB - BA);
+    }
+}
+
+}  // namespace hpkdec

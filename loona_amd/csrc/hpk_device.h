@@ -16,6 +16,7 @@ struct hpk_ctx {
     hipStream_t stream = nullptr;
     uint32_t* d_lut = nullptr;
     uint16_t* d_lo = nullptr;
+    uint8_t* d_t8 = nullptr;
     uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length
     // grow-only scratch for HPK_PTR_HOST calls
     uint8_t* d_in = nullptr;

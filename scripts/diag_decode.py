@@ -62,5 +62,8 @@ if mode == 3:
         "total_med": int(np.median(total)), "total_p90": int(np.percentile(total, 90)), "total_max": int(total.max()),
         "end_spread": int(st4[:, 2].max() - t0),
         "xcc_counts": np.bincount((st4[:, 3] >> 32).astype(np.int64), minlength=8).tolist(),
+        "end_pct": [int(x) for x in np.percentile(st4[:, 2] - t0, [0, 10, 50, 90, 99, 100])],
+        "start_pct": [int(x) for x in np.percentile(st4[:, 0] - t0, [0, 10, 50, 90, 99, 100])],
+        "dur_by_wave_in_cu": [int(np.median(total[i::16])) for i in range(16)],
     }
 print(json.dumps(res), flush=True)

@@ -1,0 +1,19 @@
+#!/usr/bin/env python3
+"""Write a decode-harness input file (bench/kvariants): u32 n, u32 enc_bytes, u32 in_off[n+1], blob."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from loona_amd import synth  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
+path = sys.argv[2] if len(sys.argv) > 2 else "/tmp/kin.bin"
+n = int(sys.argv[3]) if len(sys.argv) > 3 else None
+w = getattr(synth, cfg)() if n is None else getattr(synth, cfg)(n=n)
+with open(path, "wb") as f:
+    np.array([w.n, w.enc_bytes], np.uint32).tofile(f)
+    w.enc_off.astype(np.uint32).tofile(f)
+    w.enc_blob.tofile(f)
+print(path, w.n, w.enc_bytes)
