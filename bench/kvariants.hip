@@ -30,11 +30,11 @@ struct Dev {
     size_t out_bytes;
 };
 
-template <int kMode, int kW, int kD, int kM, int kR, int kC, int kBlocksPerCu = 1>
+template <int kMode, int kW, int kD, int kM, int kR, int kC, int kBlocksPerCu = 1, int kStep = 4>
 static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                 const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
     using G = BlockGeometry<kW, kD, kM>;
-    auto fn = hpk_decode_kernel<kMode, kW, kD, kM, kR, kC>;
+    auto fn = hpk_decode_kernel<kMode, kW, kD, kM, kR, kC, kStep>;
     const int kLdsBytes = G::kLdsBytes;
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
     dim3 grid(num_cu * kBlocksPerCu), block(G::kBlock);
@@ -132,12 +132,10 @@ int main(int argc, char** argv) {
     const int cu = prop.multiProcessorCount;
     printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
     run<0, 16, 126976, 4096, 4, 64>("b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 3, 64>("b16_r3_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 6, 64>("b16_r6_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 4, 32>("b16_r4_c32", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 4, 128>("b16_r4_c128", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 4, 256>("b16_r4_c256", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 8, 61440, 2048, 4, 64, 2>("b8x2_r4_c64_2pc", d, ref_len, ref_st, ref_out, cu, iters);
-    run<2, 16, 126976, 4096, 4, 64>("nostore_b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 4, 64, 1, 6>("s6_b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 3, 64, 1, 6>("s6_b16_r3_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 6, 64, 1, 6>("s6_b16_r6_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 8, 61440, 2048, 4, 64, 2, 6>("s6_b8x2_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
+    run<2, 16, 126976, 4096, 4, 64, 1, 6>("s6_nostore_b16_r4", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }

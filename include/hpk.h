@@ -51,7 +51,8 @@ typedef enum hpk_status {
 #define HPK_E_NODEVICE (-4) /* no GPU / kernel image for gfx950 not loadable      */
 
 /* ---- flags for batch calls --------------------------------------------- */
-#define HPK_PTR_HOST 0x0   /* all buffers are host memory: stage H2D, run, D2H, sync  */
+#define HPK_PTR_HOST 0x0   /* all buffers are host memory: staged H2D / run / D2H in overlapping
+                              chunks on the ctx's copy streams, synchronous                */
 #define HPK_PTR_DEVICE 0x1 /* all buffers are device memory: enqueue on the ctx stream */
 #define HPK_ASYNC 0x2      /* with HPK_PTR_DEVICE: return without synchronising       */
 
@@ -113,6 +114,13 @@ int hpk_decode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_
                          const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int nthreads);
 int hpk_encode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
                          const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int nthreads);
+
+/* ---- pinned host memory ---------------------------------------------------
+ * Page-lock a host range (e.g. buffet's buffer arena, crates/buffet/src/bufpool/privatepool.rs:94-108)
+ * so HPK_PTR_HOST batches inside it DMA directly and their copies overlap the kernels.
+ * Returns HPK_E_OK or HPK_E_DEVICE. */
+int hpk_host_register(void* ptr, size_t bytes);
+int hpk_host_unregister(void* ptr);
 
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);

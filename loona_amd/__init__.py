@@ -1,7 +1,7 @@
 """loona_amd — MI355X-native HPACK Huffman codec for loona's HTTP/2 header path.
 
-The product is libhpk.so (include/hpk.h C ABI; gfx950 kernels in csrc/hpk_gpu.hip). This
-package is its host-side mirror of the loona-hpack interface:
+The product is libhpk.so (include/hpk.h C ABI; gfx950 kernels in csrc/hpk_decode*.hip and
+csrc/hpk_encode.hip). This package is its host-side mirror of the loona-hpack interface:
 
     from loona_amd import HuffmanDecoder, HuffmanDecoderError, HuffmanCodec
 """

@@ -48,6 +48,8 @@ EXPORTS = (
     "hpk_encode_batch",
     "hpk_decode_batch_cpu",
     "hpk_encode_batch_cpu",
+    "hpk_host_register",
+    "hpk_host_unregister",
     "hpk_version",
 )
 
@@ -102,6 +104,10 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
             fn.restype = ctypes.c_int
+        L.hpk_host_register.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.hpk_host_register.restype = ctypes.c_int
+        L.hpk_host_unregister.argtypes = [ctypes.c_void_p]
+        L.hpk_host_unregister.restype = ctypes.c_int
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

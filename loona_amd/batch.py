@@ -221,3 +221,29 @@ def decode_offsets_torch(in_off):
 
 def encode_offsets_torch(in_off):
     return _bound_offsets_torch(in_off, 30, 8, 7)
+
+
+def _cpu_batch(fn_name, bound, in_blob, in_off, nthreads):
+    L = _lib.lib()
+    in_blob = np.ascontiguousarray(in_blob, dtype=np.uint8)
+    in_off = np.ascontiguousarray(in_off, dtype=U32)
+    out_off = bound(in_off)
+    n = len(in_off) - 1
+    out_blob = np.zeros(max(int(out_off[-1]), 1), dtype=np.uint8)
+    out_len = np.zeros(max(n, 1), dtype=U32)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    src = in_blob if in_blob.size else np.zeros(1, dtype=np.uint8)
+    rc = getattr(L, fn_name)(src.ctypes.data, in_off.ctypes.data, n, out_blob.ctypes.data, out_off.ctypes.data,
+                             out_len.ctypes.data, status.ctypes.data, int(nthreads))
+    _lib.check(rc, fn_name)
+    return out_blob, out_off, out_len[:n], status[:n]
+
+
+def decode_batch_cpu(in_blob, in_off, nthreads=0):
+    """The library's table-driven CPU batch decode (hpk_decode_batch_cpu): same layout and
+    results as the device path, host threads over byte-balanced shards."""
+    return _cpu_batch("hpk_decode_batch_cpu", decode_offsets_np, in_blob, in_off, nthreads)
+
+
+def encode_batch_cpu(in_blob, in_off, nthreads=0):
+    return _cpu_batch("hpk_encode_batch_cpu", encode_offsets_np, in_blob, in_off, nthreads)

@@ -50,7 +50,6 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     c->num_cu = prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", e);
     c->stream = c->own;
-    if ((e = hipMalloc(&c->d_lut, sizeof(t->lut))) != hipSuccess) return fail("hipMalloc lut", e);
     if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
     if ((e = hipMalloc(&c->d_t8, sizeof(t->t8))) != hipSuccess) return fail("hipMalloc t8", e);
     if ((e = hipMemcpy(c->d_t8, t->t8, sizeof(t->t8), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload t8", e);
@@ -60,7 +59,6 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
         packed[s] = t->code[s];
         packed[257 + s] = t->len[s];
     }
-    if ((e = hipMemcpy(c->d_lut, t->lut, sizeof(t->lut), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload lut", e);
     if ((e = hipMemcpy(c->d_lo, t->lo, sizeof(t->lo), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload lo", e);
     if ((e = hipMemcpy(c->d_codes, packed, sizeof(packed), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload codes", e);
     return c;
@@ -70,7 +68,6 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->d_lut);
     (void)hipFree(c->d_lo);
     (void)hipFree(c->d_t8);
     (void)hipFree(c->d_codes);
@@ -78,6 +75,12 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
+    for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
+        if (c->ev_in[j]) (void)hipEventDestroy(c->ev_in[j]);
+        if (c->ev_run[j]) (void)hipEventDestroy(c->ev_run[j]);
+    }
+    if (c->h2d) (void)hipStreamDestroy(c->h2d);
+    if (c->d2h) (void)hipStreamDestroy(c->d2h);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -88,6 +91,18 @@ extern "C" int hpk_ctx_set_stream(hpk_ctx* c, void* s) {
         c->stream = (hipStream_t)0;
     else
         c->stream = s ? (hipStream_t)s : c->own;
+    return HPK_E_OK;
+}
+
+extern "C" int hpk_host_register(void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return hpk_set_err_msg("null range", HPK_E_INVAL);
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return HPK_E_OK;
+}
+
+extern "C" int hpk_host_unregister(void* ptr) {
+    if (!ptr) return hpk_set_err_msg("null pointer", HPK_E_INVAL);
+    HIP_TRY(hipHostUnregister(ptr));
     return HPK_E_OK;
 }
 
@@ -144,14 +159,54 @@ static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uin
     uint32_t* d_in_off = c->d_meta;
     uint32_t* d_out_off = c->d_meta + (n + 1);
     uint32_t* d_len = c->d_meta + 2 * ((size_t)n + 1);
-    if (in_bytes) HIP_TRY(hipMemcpyAsync(c->d_in, in_blob, in_bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_in_off, in_off, (n + 1) * 4ull, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(d_out_off, out_off, (n + 1) * 4ull, hipMemcpyHostToDevice, c->stream));
-    if ((rc = fn(c, c->d_in, d_in_off, n, c->d_out, d_out_off, d_len, c->d_st))) return rc;
-    if (out_bytes) HIP_TRY(hipMemcpyAsync(out_blob, c->d_out, out_bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(out_len, d_len, n * 4ull, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(status, c->d_st, n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // Pipeline: the batch is cut into up to kMaxChunks literal ranges balanced by encoded bytes;
+    // chunk j's copy-in (h2d stream), kernel (ctx stream) and copy-out (d2h stream) overlap with
+    // the neighbouring chunks' (PCIe is full duplex). Offsets stay absolute, so every chunk is
+    // the same kernel on a sub-range of the scratch buffers. With pageable host memory HIP
+    // stages the copies itself and the overlap is small: register the arena (hpk_host_register).
+    if (!c->h2d) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
+        for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_in[j], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_run[j], hipEventDisableTiming));
+        }
+    }
+    const size_t kChunkBytes = (size_t)4 << 20;
+    int chunks = (int)((in_bytes + out_bytes) / kChunkBytes);
+    chunks = chunks < 1 ? 1 : (chunks > hpk_ctx::kMaxChunks ? hpk_ctx::kMaxChunks : chunks);
+    if ((uint32_t)chunks > n) chunks = (int)n;
+    uint32_t cut[hpk_ctx::kMaxChunks + 1];
+    cut[0] = 0;
+    for (int j = 1; j < chunks; ++j) {  // first literal whose end passes j/chunks of the bytes
+        const uint64_t target = (uint64_t)in_bytes * j / chunks;
+        uint32_t lo = cut[j - 1], hi = n;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (in_off[mid + 1] < target) lo = mid + 1; else hi = mid;
+        }
+        cut[j] = lo;
+    }
+    cut[chunks] = n;
+    HIP_TRY(hipEventRecord(c->ev_run[0], c->stream));  // earlier work on the ctx stream first
+    HIP_TRY(hipStreamWaitEvent(c->h2d, c->ev_run[0], 0));
+    for (int j = 0; j < chunks; ++j) {
+        const uint32_t a = cut[j], b = cut[j + 1];
+        if (a == b) continue;
+        const size_t ib = in_off[a], ie = in_off[b], ob = out_off[a], oe = out_off[b];
+        if (ie > ib) HIP_TRY(hipMemcpyAsync(c->d_in + ib, in_blob + ib, ie - ib, hipMemcpyHostToDevice, c->h2d));
+        HIP_TRY(hipMemcpyAsync(d_in_off + a, in_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
+        HIP_TRY(hipMemcpyAsync(d_out_off + a, out_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
+        HIP_TRY(hipEventRecord(c->ev_in[j], c->h2d));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_in[j], 0));
+        if ((rc = fn(c, c->d_in, d_in_off + a, b - a, c->d_out, d_out_off + a, d_len + a, c->d_st + a))) return rc;
+        HIP_TRY(hipEventRecord(c->ev_run[j], c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->d2h, c->ev_run[j], 0));
+        if (oe > ob) HIP_TRY(hipMemcpyAsync(out_blob + ob, c->d_out + ob, oe - ob, hipMemcpyDeviceToHost, c->d2h));
+        HIP_TRY(hipMemcpyAsync(out_len + a, d_len + a, (b - a) * 4ull, hipMemcpyDeviceToHost, c->d2h));
+        HIP_TRY(hipMemcpyAsync(status + a, c->d_st + a, b - a, hipMemcpyDeviceToHost, c->d2h));
+    }
+    HIP_TRY(hipStreamSynchronize(c->d2h));
     return HPK_E_OK;
 }
 

@@ -185,6 +185,98 @@ __device__ __forceinline__ void lit_step(Lit& L, const Src& src, const uint8_t* 
     }
 }
 
+// Append g (<= 4) bytes to the pending output, garbage-tolerant: bytes of acc above the accn
+// valid ones may hold anything (they are masked here before new bytes land on them, and the
+// final partial dword only writes inside the literal's own output region, whose bytes past
+// out_len are unspecified by the ABI).
+template <int kStore>
+__device__ __forceinline__ void lit_emit_g(Lit& L, uint32_t packed, uint32_t g, uint8_t* __restrict__ out8) {
+    const uint32_t sh = 8u * L.accn;  // accn <= 3 here
+    const uint64_t add = (uint64_t)packed << sh;
+    const uint32_t lo = ((uint32_t)L.acc & __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, sh)) | (uint32_t)add;
+    L.acc = ((uint64_t)(uint32_t)(add >> 32) << 32) | lo;
+    L.accn += g;
+    L.cnt += g;
+    if (L.accn >= 4u) {
+        if (kStore == kDword) {
+            reinterpret_cast<uint32_t*>(out8)[L.od] = (uint32_t)L.acc;
+        } else if (kStore == kChecked) {
+            if (L.od < L.oend)
+                reinterpret_cast<uint32_t*>(out8)[L.od] = (uint32_t)L.acc;
+            else
+                chk_report(1, L.od, L.oend, L.cnt);
+        } else {
+            asm volatile("" ::"v"((uint32_t)L.acc));
+        }
+        L.od += 1;
+        L.acc >>= 32;
+        L.accn -= 4u;
+    }
+}
+
+// v6 step: the same speculative 4-code decode as lit_step, in 32-bit arithmetic. Code i starts
+// at bit c_i = 5i + e_i of the window's top dword (e_i = extra bits of codes 0..i-1 over 5).
+// Its 5-bit prefix t_i alone fixes the 5..8-bit length (the canonical limits 0x50/0xB8/0xF8
+// end in three zero bits, i.e. t >= 10, 23, 31), so len_i - 5 = popcount(M << (31 - t_i)) with
+// M = bits {10, 23, 31}, and 31 - t_i is a bit-field extract of ~hi pre-shifted by 5i: the
+// serial chain per code is extract, shift, popcount, subtract. Symbols and the fast test read
+// the 8-bit prefix off the chain. f_i = 27 - e_i.
+template <int kStore, class Src>
+__device__ __forceinline__ void lit_step6(Lit& L, const Src& src, const uint8_t* __restrict__ t8,
+                                          const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8) {
+    lit_refill(L, src);
+    constexpr uint32_t M = (1u << 10) | (1u << 23) | (1u << 31);
+    const uint32_t hi = (uint32_t)(L.win >> 32);
+    const uint32_t nh = ~hi;
+    uint32_t f[5], sym[4];
+    bool fast[4], fits[4];
+    f[0] = 27;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = __builtin_amdgcn_ubfe(nh << (5 * i), f[i], 5);  // 31 - t_i
+        f[i + 1] = f[i] - (uint32_t)__builtin_popcount(M << s);
+        const uint32_t b = __builtin_amdgcn_ubfe(hi, f[i] - (3 + 5 * i), 8);
+        fast[i] = b < 0xFEu;
+        sym[i] = t8[b];
+        // code i ends inside the literal: c_{i+1} = 5(i+1) + 27 - f_{i+1} <= rem
+        fits[i] = f[i + 1] + L.rem >= 32u + 5u * i;
+    }
+    const bool m0 = L.live && fast[0] && fits[0];
+    const bool m1 = m0 && fast[1] && fits[1];
+    const bool m2 = m1 && fast[2] && fits[2];
+    const bool m3 = m2 && fast[3] && fits[3];
+    const uint32_t g = (uint32_t)m0 + (uint32_t)m1 + (uint32_t)m2 + (uint32_t)m3;
+    const uint32_t fg = m3 ? f[4] : m2 ? f[3] : m1 ? f[2] : m0 ? f[1] : 27u;
+    const uint32_t use = 5u * g + 27u - fg;
+    const bool bad_fast = m2 ? fast[3] : m1 ? fast[2] : m0 ? fast[1] : fast[0];
+    const bool park = L.live && !m3 && !bad_fast;
+    L.win <<= use;
+    L.nb -= use;
+    L.rem -= use;
+    const uint32_t packed = sym[0] | (sym[1] << 8) | (sym[2] << 16) | (sym[3] << 24);
+    lit_emit_g<kStore>(L, packed, g, out8);
+    L.live = park || (m3 && L.rem != 0u);
+    if (park) {  // a 10..30-bit code (or EOS): one lookup in the leading-ones table
+        lit_refill(L, src);
+        const uint32_t w = (uint32_t)(L.win >> 32);
+        uint32_t s1, len;
+        bool eos;
+        lo_decode(w, lo, s1, len, eos);
+        if (len > L.rem) {
+            L.live = false;  // only padding left
+        } else if (eos) {
+            L.st = HPK_EOS_IN_STRING;  // huffman.rs:112-116
+            L.live = false;
+        } else {
+            L.win <<= len;
+            L.nb -= len;
+            L.rem -= len;
+            lit_emit_g<kStore>(L, s1, 1u, out8);
+            L.live = L.rem != 0u;
+        }
+    }
+}
+
 template <int kStore>
 __device__ __forceinline__ void lit_finish(Lit& L, const DecodeArgs& a, uint32_t i) {
     // the last, partial dword lies inside this literal's capacity (aligned, >= decoded bound)
@@ -278,7 +370,7 @@ constexpr uint32_t kQByte = 0x80000000u;  // queue entry .y flag: byte path
 // kMode: 0 = product kernel; diagnostic variants (HPK_DEBUG_MODE, never the default):
 //   1 = stage only (no decode), 2 = decode without output stores, 3 = product + per-wave stamps,
 //   4 = every global store bounds-checked (first violation recorded in g_chk, store skipped)
-template <int kMode, int kWaves, int kData, int kMaxLits, int kRefillN, int kChunk>
+template <int kMode, int kWaves, int kData, int kMaxLits, int kRefillN, int kChunk, int kStep = 4>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode_kernel(DecodeArgs a) {
     using G = BlockGeometry<kWaves, kData, kMaxLits>;
     unsigned long long t_start = 0, t_staged = 0;
@@ -398,7 +490,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode_kernel(DecodeArgs a) {
             begin(t);
             for (;;) {
 #pragma unroll
-                for (int s = 0; s < kRefillN; ++s) lit_step<kStore>(L, lds, s_t8, s_lo, a.out_base);
+                for (int s = 0; s < kRefillN; ++s) {
+                    if (kStep == 6)
+                        lit_step6<kStore>(L, lds, s_t8, s_lo, a.out_base);
+                    else
+                        lit_step<kStore>(L, lds, s_t8, s_lo, a.out_base);
+                }
                 const bool fin = t < k && !L.live;
                 if (__any(fin)) {
                     if (fin && act) lit_finish<kStore>(L, a, cur + t);

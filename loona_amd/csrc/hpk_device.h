@@ -14,7 +14,6 @@ struct hpk_ctx {
     int num_cu = 256;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    uint32_t* d_lut = nullptr;
     uint16_t* d_lo = nullptr;
     uint8_t* d_t8 = nullptr;
     uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length
@@ -27,6 +26,12 @@ struct hpk_ctx {
     size_t d_meta_cap = 0;
     uint8_t* d_st = nullptr;
     size_t d_st_cap = 0;
+    // host-pointer pipeline: copy-in and copy-out streams + per-chunk events (created lazily)
+    static constexpr int kMaxChunks = 8;
+    hipStream_t h2d = nullptr;
+    hipStream_t d2h = nullptr;
+    hipEvent_t ev_in[kMaxChunks] = {};
+    hipEvent_t ev_run[kMaxChunks] = {};
 };
 
 int hpk_set_err(const char* what, hipError_t e);

@@ -184,3 +184,26 @@ def test_config3_roundtrip_sample(codec):
     dl = d[2].astype(np.int64)
     idx = np.repeat(d[1][:-1].astype(np.int64) - (np.cumsum(dl) - dl), dl) + np.arange(int(dl.sum()))
     assert np.array_equal(d[0][idx], w.dec_blob)
+
+
+def test_host_pointer_mode_pipelined(codec):
+    """HPK_PTR_HOST at a size that takes the chunked copy/decode pipeline (8 chunks), from
+    pageable and from page-locked (hpk_host_register) buffers: identical to the device path."""
+    from loona_amd import _lib, synth
+
+    w = synth.config2(n=300_000, seed=99)
+    ref = gpu_decode(codec, w.enc_blob, w.enc_off)
+    got = codec.decode_host(w.enc_blob, w.enc_off)
+    compare_batches(got, ref, "host pipelined vs device")
+    L = _lib.lib()
+    blob = np.ascontiguousarray(w.enc_blob)
+    assert L.hpk_host_register(blob.ctypes.data, blob.nbytes) == 0
+    try:
+        got = codec.decode_host(blob, w.enc_off)
+    finally:
+        assert L.hpk_host_unregister(blob.ctypes.data) == 0
+    compare_batches(got, ref, "host pipelined (pinned) vs device")
+    # encode through the same pipeline round-trips
+    e = codec.encode_host(w.dec_blob, w.dec_off)
+    assert not e[3].any()
+    assert np.array_equal(e[2].astype(np.int64), np.diff(w.enc_off.astype(np.int64)))
