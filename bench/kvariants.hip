@@ -30,23 +30,21 @@ struct Dev {
     size_t out_bytes;
 };
 
-template <int kMode, int kW, int kD, int kM, int kR, int kC, int kBlocksPerCu = 1, int kStep = 4>
-static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
-                const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
-    using G = BlockGeometry<kW, kD, kM>;
-    auto fn = hpk_decode_kernel<kMode, kW, kD, kM, kR, kC, kStep>;
-    const int kLdsBytes = G::kLdsBytes;
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
-    dim3 grid(num_cu * kBlocksPerCu), block(G::kBlock);
+template <int kMode, class Fn>
+static void run_fn(const char* name, Fn fn, int lds, int block, int blocks_per_cu, Dev& d,
+                   const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
+                   const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    dim3 grid(num_cu * blocks_per_cu), blk(block);
     CK(hipMemset(d.a.out_len, 0xFF, d.n * 4));
     CK(hipMemset(d.a.out_base, 0xAB, d.out_bytes));
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, grid, block, kLdsBytes, 0, d.a);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, grid, blk, lds, 0, d.a);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(fn, grid, block, kLdsBytes, 0, d.a);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(fn, grid, blk, lds, 0, d.a);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -59,7 +57,6 @@ static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, 
     size_t bad = 0;
     for (uint32_t i = 0; i < d.n; ++i)
         if (len[i] != ref_len[i] || st[i] != ref_st[i]) ++bad;
-    // compare valid bytes
     std::vector<uint32_t> oo(d.n + 1);
     CK(hipMemcpy(oo.data(), d.a.out_off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
     size_t badb = 0;
@@ -69,6 +66,24 @@ static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, 
     printf("{\"variant\": \"%s\", \"us\": %.2f, \"bad_len_status\": %zu, \"bad_bytes\": %zu}\n", name,
            ms * 1000.0 / iters, bad, badb);
     fflush(stdout);
+}
+
+// v5: block window + block queue, output stored straight to global
+template <int kMode, int kW, int kD, int kM, int kR, int kC, int kBlocksPerCu = 1, int kStep = 4>
+static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
+                const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
+    using G = BlockGeometry<kW, kD, kM>;
+    run_fn<kMode>(name, hpk_decode_kernel<kMode, kW, kD, kM, kR, kC, kStep>, G::kLdsBytes, G::kBlock, kBlocksPerCu, d,
+                  ref_len, ref_st, ref_out, num_cu, iters);
+}
+
+// v7: input window + output image in LDS, longest-first queue
+template <int kMode, int kWaves, int kW, int kO, int kQ, int kR, int kC, int kStep, int kBlocksPerCu = 1>
+static void run7(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
+                 const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
+    using G = Geo7<kWaves, kW, kO, kQ>;
+    run_fn<kMode>(name, hpk_decode7<kMode, kWaves, kW, kO, kQ, kR, kC, kStep>, G::kLdsBytes, G::kBlock, kBlocksPerCu,
+                  d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
 extern "C" int hpk_decode_batch_cpu(const uint8_t*, const uint32_t*, uint32_t, uint8_t*, const uint32_t*, uint32_t*,
@@ -131,11 +146,13 @@ int main(int argc, char** argv) {
     CK(hipGetDeviceProperties(&prop, 0));
     const int cu = prop.multiProcessorCount;
     printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
-    run<0, 16, 126976, 4096, 4, 64>("b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 4, 64, 1, 6>("s6_b16_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 3, 64, 1, 6>("s6_b16_r3_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 16, 126976, 4096, 6, 64, 1, 6>("s6_b16_r6_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<0, 8, 61440, 2048, 4, 64, 2, 6>("s6_b8x2_r4_c64", d, ref_len, ref_st, ref_out, cu, iters);
-    run<2, 16, 126976, 4096, 4, 64, 1, 6>("s6_nostore_b16_r4", d, ref_len, ref_st, ref_out, cu, iters);
+    run<0, 16, 126976, 4096, 4, 64, 1, 6>("v5_s6", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 4, 64, 6>("v7_s6_r4", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 4, 64, 4>("v7_s4_r4", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 3, 64, 6>("v7_s6_r3", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 6, 64, 6>("v7_s6_r6", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 8, 22528, 43008, 1024, 4, 64, 6, 2>("v7_w8x2_s6_r4", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<2, 16, 45056, 86016, 2048, 4, 64, 6>("v7_nostore", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<1, 16, 45056, 86016, 2048, 4, 64, 6>("v7_stage_flush", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }

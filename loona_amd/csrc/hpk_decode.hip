@@ -33,11 +33,12 @@
 
 using namespace hpkdec;
 
-// Product geometry: 16 waves (one 1024-thread workgroup) per CU sharing a 124 KiB literal window
-// and a 4096-entry queue; lanes refill every 4 steps (chosen with bench/kvariants).
-constexpr int kWaves = 16, kData = 126976, kMaxLits = 4096, kRefillN = 4, kChunk = 64;
-using Geo = BlockGeometry<kWaves, kData, kMaxLits>;
-#define DEC_KERNEL(m) hpk_decode_kernel<m, kWaves, kData, kMaxLits, kRefillN, kChunk>
+// Product geometry (v7): 16 waves (one 1024-thread workgroup) per CU; per fill a 44 KiB input
+// window, an 84 KiB output image and a 2048-entry longest-first queue; lanes refill every 4
+// steps, waves reserve 64 queue slots at a time (chosen with bench/kvariants).
+constexpr int kWaves = 16, kW = 45056, kO = 86016, kQ = 2048, kRefillN = 4, kChunk = 64, kStep = 6;
+using Geo = Geo7<kWaves, kW, kO, kQ>;
+#define DEC_KERNEL(m) hpk_decode7<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kStep>
 
 static int g_debug_mode = -1;
 
@@ -86,8 +87,8 @@ int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
     a.in_off = in_off;
     a.n = n;
     const uintptr_t op = (uintptr_t)out_blob;
-    a.out_base = (uint8_t*)(op & ~(uintptr_t)3);
-    a.out_mis = (uint32_t)(op & 3);
+    a.out_base = (uint8_t*)(op & ~(uintptr_t)15);
+    a.out_mis = (uint32_t)(op & 15);
     a.out_off = out_off;
     a.out_len = out_len;
     a.status = status;

@@ -18,8 +18,8 @@ struct DecodeArgs {
     uint32_t in_mis;         // in_blob - in_base (0..15)
     const uint32_t* in_off;
     uint32_t n;
-    uint8_t* out_base;  // out_blob rounded down to 4 bytes
-    uint32_t out_mis;   // out_blob - out_base (0..3)
+    uint8_t* out_base;  // out_blob rounded down to 16 bytes
+    uint32_t out_mis;   // out_blob - out_base (0..15)
     const uint32_t* out_off;
     uint32_t* out_len;
     uint8_t* status;
@@ -277,6 +277,21 @@ __device__ __forceinline__ void lit_step6(Lit& L, const Src& src, const uint8_t*
     }
 }
 
+// Final status of a literal whose walk has stopped (huffman.rs:128-160): at most 7 residual
+// bits, all ones (the most significant bits of EOS); an EOS decoded inside wins (st already set).
+__device__ __forceinline__ uint32_t lit_status(const Lit& L) {
+    uint32_t st = L.st;
+    if (st == HPK_OK && L.rem > 0) {
+        if (L.rem > 7) {
+            st = HPK_PADDING_TOO_LARGE;
+        } else {
+            const uint32_t w = (uint32_t)(L.win >> 32) | (0xFFFFFFFFu >> L.rem);
+            if (w != 0xFFFFFFFFu) st = HPK_INVALID_PADDING;
+        }
+    }
+    return st;
+}
+
 template <int kStore>
 __device__ __forceinline__ void lit_finish(Lit& L, const DecodeArgs& a, uint32_t i) {
     // the last, partial dword lies inside this literal's capacity (aligned, >= decoded bound)
@@ -291,15 +306,7 @@ __device__ __forceinline__ void lit_finish(Lit& L, const DecodeArgs& a, uint32_t
         chk_report(3, i, a.n, 0);
         return;
     }
-    uint32_t st = L.st;
-    if (st == HPK_OK && L.rem > 0) {  // huffman.rs:128-160: at most 7 bits, all ones (EOS MSBs)
-        if (L.rem > 7) {
-            st = HPK_PADDING_TOO_LARGE;
-        } else {
-            const uint32_t w = (uint32_t)(L.win >> 32) | (0xFFFFFFFFu >> L.rem);
-            if (w != 0xFFFFFFFFu) st = HPK_INVALID_PADDING;
-        }
-    }
+    const uint32_t st = lit_status(L);
     a.out_len[i] = L.cnt;
     a.status[i] = (uint8_t)st;
 }
@@ -534,6 +541,386 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode_kernel(DecodeArgs a) {
             }
         }
         cur += k;
+    }
+    if (kMode == 3 && lane == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        const uint64_t gwi = (uint64_t)blockIdx.x * kWaves + (tid >> 6);
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.dbg[gwi * 4 + 0] = t_start;
+        a.dbg[gwi * 4 + 1] = t_staged;
+        a.dbg[gwi * 4 + 2] = t_end;
+        a.dbg[gwi * 4 + 3] = ((unsigned long long)xcc << 32) | (BB - BA);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// v7: output staged in LDS too, queue in longest-first order.
+//
+// PMC on v5 showed 163 MB of HBM writes per launch for 41 MB of output: every lane stores its
+// own literal's dwords whenever they complete, so a 64-B sector is written several times (by
+// the lane itself as the L2 evicts the half-written line, and by the neighbouring literal's
+// lane at the boundary). Here each fill decodes into an LDS image of its output span and the
+// workgroup writes the span back with 16-byte stores, exact bytes; out_len and status are
+// staged and written back coalesced as well. LDS is then shared by an input window, the
+// output image (1.6x + rounding) and the queue, so fills are ~2.5x smaller; the load balance
+// that costs is won back by ordering each fill's queue longest-first (a counting sort on the
+// encoded length: LPT list scheduling, the tail is made of short literals).
+template <int kWaves, int kW, int kO, int kQ>
+struct Geo7 {
+    static constexpr int kBlock = kWaves * 64;
+    static constexpr int kMetaRounds = (kQ + kBlock - 1) / kBlock;
+    static constexpr int kStageRounds = (kW / 16 + kBlock - 1) / kBlock;
+    static constexpr int kFlushRounds = (kO / 16 + 1 + kBlock - 1) / kBlock;
+    static constexpr int kInOff = kTabBytes;
+    static constexpr int kOutOff = kInOff + kW;
+    static constexpr int kQOff = kOutOff + kO;
+    static constexpr int kLenOff = kQOff + 8 * kQ;
+    static constexpr int kHistOff = kLenOff + 4 * kQ;  // 64 bucket counts + 64 bucket bases
+    static constexpr int kCtrOff = kHistOff + 512;
+    static constexpr int kLdsBytes = kCtrOff + 16;
+    static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+    static_assert(kW % 16 == 0 && kW <= 65536, "window offsets and lengths pack in 16 bits");
+    static_assert(kO % 16 == 0 && kO / 4 <= 32768, "output dword index packs in 15 bits");
+    static_assert(kQ <= 4096, "fill index packs in 12 bits");
+};
+constexpr uint32_t kQ7Byte = 0x80000000u;  // queue entry .y flag: byte path
+
+// Longest-first bucket of an encoded length (0 = longest): 2-byte classes up to 94 B, then
+// 128-byte classes.
+__device__ __forceinline__ uint32_t lpt_bucket(uint32_t nbytes) {
+    const uint32_t b = nbytes < 96u ? (nbytes >> 1) : min(63u, 48u + ((nbytes - 96u) >> 7));
+    return 63u - b;
+}
+
+// One literal decoded code by code into a byte destination with a capacity check per byte.
+template <class Src, class Dst>
+__device__ __forceinline__ void lit_bytes_to(Lit& L, const Src& src, const uint16_t* lo, Dst dst, uint32_t ocap,
+                                             uint32_t sb, uint32_t nbytes) {
+    lit_begin(L, src, sb, nbytes);
+    while (L.live) {
+        lit_refill(L, src);
+        uint32_t sym, len;
+        bool eos;
+        lo_decode((uint32_t)(L.win >> 32), lo, sym, len, eos);
+        if (len > L.rem) break;
+        if (eos) {
+            L.st = HPK_EOS_IN_STRING;
+            break;
+        }
+        if (L.cnt >= ocap) {
+            L.st = HPK_OUTPUT_OVERFLOW;
+            break;
+        }
+        dst(L.cnt, (uint8_t)sym);
+        L.cnt += 1;
+        L.win <<= len;
+        L.nb -= len;
+        L.rem -= len;
+        L.live = L.rem != 0u;
+    }
+}
+
+// Workgroup barrier that orders LDS only: outstanding global stores (the previous fill's
+// write-back) and prefetch loads stay in flight across it. __syncthreads() would wait for them.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Registers of the next fill, loaded while the current one decodes: the offsets of up to kQ
+// literals and the whole kW-byte input window (clamped to the batch).
+template <int kMeta, int kStage>
+struct Prefetch {
+    uint32_t io0[kMeta], io1[kMeta], oo0[kMeta], oo1[kMeta];
+    uint4 chunk[kStage];
+};
+
+template <int kBlock, int kMeta, int kStage>
+__device__ __forceinline__ void prefetch_fill(Prefetch<kMeta, kStage>& P, const DecodeArgs& a, uint32_t tid,
+                                              uint32_t cur, uint32_t end, uint32_t base16, uint32_t last16) {
+    const uint32_t cntl = end - cur;  // >= 1
+#pragma unroll
+    for (int r = 0; r < kMeta; ++r) {
+        const uint32_t t = min(tid + (uint32_t)kBlock * r, cntl - 1);
+        P.io0[r] = a.in_off[cur + t];
+        P.io1[r] = a.in_off[cur + t + 1];
+        P.oo0[r] = a.out_off[cur + t];
+        P.oo1[r] = a.out_off[cur + t + 1];
+    }
+    const uint4* g16 = reinterpret_cast<const uint4*>(a.in_base);
+#pragma unroll
+    for (int r = 0; r < kStage; ++r) P.chunk[r] = g16[min((base16 >> 4) + tid + (uint32_t)kBlock * r, last16)];
+}
+
+// kMode as for v5 (0 product, 1 stage+flush only, 2 no output stores, 3 stamps, 4 checked).
+//
+// Software pipeline across fills: while fill j decodes, fill j+1's offsets and input window are
+// already in flight into registers, and fill j-1's write-back stores drain; only LDS work
+// (queue build, window copy, flush reads) sits between two decodes.
+template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kStep>
+__global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
+    using G = Geo7<kWaves, kW, kO, kQ>;
+    constexpr int R = G::kMetaRounds, S = G::kStageRounds;
+    unsigned long long t_start = 0, t_staged = 0;
+    if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* s_t8 = smem;
+    uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
+    uint8_t* s_in = smem + G::kInOff;
+    uint8_t* s_out = smem + G::kOutOff;
+    uint32_t* s_out32 = reinterpret_cast<uint32_t*>(s_out);
+    uint2* s_q = reinterpret_cast<uint2*>(smem + G::kQOff);
+    uint32_t* s_lenst = reinterpret_cast<uint32_t*>(smem + G::kLenOff);  // len | status << 24
+    uint32_t* s_hist = reinterpret_cast<uint32_t*>(smem + G::kHistOff);
+    uint32_t* s_bbase = s_hist + 64;
+    // [0] fitting count, [1] queue head, [2] input end of the fill, [3] output end of the fill
+    uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);
+    for (uint32_t t = threadIdx.x; t < kT8Bytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_t8)[t] = reinterpret_cast<const uint4*>(a.t8)[t];
+    for (uint32_t t = threadIdx.x; t < kLoBytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const LdsSrc lds{reinterpret_cast<const uint32_t*>(s_in)};
+    const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
+    const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+    const uint32_t in_end = a.in_off[a.n] + a.in_mis;
+    const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
+
+    // write back one decoded fill from the LDS image: the output span [G0, G1) with 16-byte
+    // stores (bytewise in the two end chunks, which neighbours own), then out_len and status
+    auto flush = [&](uint32_t fcur, uint32_t fk, uint32_t G0, uint32_t G1) {
+        const uint32_t ob = G0 & ~15u;
+        if (kMode != 2) {
+            const uint32_t c0 = ob >> 4, c1 = (G1 + 15) >> 4;
+            const uint4* l16 = reinterpret_cast<const uint4*>(s_out);
+            uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
+#pragma unroll
+            for (int r = 0; r < G::kFlushRounds; ++r) {
+                const uint32_t ci = c0 + tid + (uint32_t)G::kBlock * r;
+                if (ci < c1 && (ci << 4) >= G0 && (ci << 4) + 16u <= G1) g16[ci] = l16[ci - c0];
+            }
+            if (tid < 2) {  // the partial chunks at the two ends
+                const uint32_t g = tid == 0 ? c0 << 4 : (c1 - 1) << 4;
+                if (!(g >= G0 && g + 16u <= G1) && (tid == 0 || c1 - 1 != c0)) {
+#pragma unroll 1
+                    for (uint32_t b = 0; b < 16u; ++b)
+                        if (g + b >= G0 && g + b < G1) a.out_base[g + b] = s_out[g + b - ob];
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = tid + (uint32_t)G::kBlock * r;
+            if (i < fk) {
+                const uint32_t v = s_lenst[i];
+                a.out_len[fcur + i] = v & 0xFFFFFFu;
+                a.status[fcur + i] = (uint8_t)(v >> 24);
+            }
+        }
+    };
+    uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
+
+    uint32_t cur = BA;
+    uint32_t gin = 0, gout = 0;  // exact input / output start of the fill (blob-relative + mis)
+    Prefetch<R, S> P;
+    if (cur < BB) {
+        gin = a.in_off[cur] + a.in_mis;
+        gout = a.out_off[cur] + a.out_mis;
+        prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, last16);
+    }
+    while (cur < BB) {  // block-uniform
+        const uint32_t cntl = min((uint32_t)kQ, BB - cur);
+        const uint32_t base16 = gin & ~15u;
+        const uint32_t ob16 = gout & ~15u;
+        lds_barrier();  // previous fill decoded and its image read out: every LDS region is free
+        if (tid < 64) s_hist[tid] = 0;
+        if (tid == 0) {
+            s_ctr[0] = 0;
+            s_ctr[1] = G::kBlock;
+            s_ctr[2] = gin;
+            s_ctr[3] = gout;
+        }
+        lds_barrier();
+        uint32_t ex[R], ey[R], pos[R];
+        uint32_t kw = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
+            const uint32_t o0 = P.oo0[r] + a.out_mis, o1 = P.oo1[r] + a.out_mis;
+            // fitting literals form a prefix (offsets are non-decreasing)
+            const bool fits = t < cntl && p1 - base16 <= (uint32_t)kW && o1 - ob16 <= (uint32_t)kO;
+            pos[r] = 0xFFFFFFFFu;
+            if (fits) {
+                const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
+                // dword path: aligned region holding hpk_decoded_bound(nbytes) bytes
+                const bool dw = ((o0 | ocap) & 3u) == 0 && ocap >= (nbytes * 8u) / 5u;
+                ex[r] = (p0 - base16) | (nbytes << 16);
+                ey[r] = t | (((o0 - ob16) >> 2) << 12) | (dw ? 0u : kQ7Byte);
+                const uint32_t bk = lpt_bucket(nbytes);
+                pos[r] = (bk << 16) | atomicAdd(&s_hist[bk], 1u);
+            }
+            const uint64_t fb = __ballot(fits);
+            kw += (uint32_t)__popcll(fb);
+            if (fb) {  // the wave's last fitting literal ends furthest (offsets non-decreasing)
+                const int hl = 63 - __builtin_clzll(fb);
+                const uint32_t e_in = (uint32_t)__builtin_amdgcn_readlane((int)p1, hl);
+                const uint32_t e_out = (uint32_t)__builtin_amdgcn_readlane((int)o1, hl);
+                if (lane == 0) {
+                    atomicMax(&s_ctr[2], e_in);
+                    atomicMax(&s_ctr[3], e_out);
+                }
+            }
+        }
+        if (lane == 0 && kw) atomicAdd(&s_ctr[0], kw);
+        lds_barrier();
+        const uint32_t k = s_ctr[0];
+        if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global
+            if (tid == 0) {
+                const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), last16 * 4 + 3};
+                uint8_t* dst = a.out_base + gout;
+                Lit L = {};
+                lit_bytes_to(L, g, s_lo, [&](uint32_t j, uint8_t v) { dst[j] = v; },
+                             a.out_off[cur + 1] - a.out_off[cur], gin, a.in_off[cur + 1] + a.in_mis - gin);
+                a.out_len[cur] = L.cnt;
+                a.status[cur] = (uint8_t)lit_status(L);
+            }
+            cur += 1;
+            if (cur < BB) {
+                gin = a.in_off[cur] + a.in_mis;
+                gout = a.out_off[cur] + a.out_mis;
+                prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, last16);
+            }
+            continue;
+        }
+        const uint32_t gin_next = s_ctr[2], gout_next = s_ctr[3];  // = in/out offsets of cur + k
+        // bucket bases (exclusive scan over 64 buckets by wave 0), then scatter the entries
+        if (tid < 64) {
+            const uint32_t v = s_hist[tid];
+            uint32_t x = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= (uint32_t)d) x += y;
+            }
+            s_bbase[tid] = x - v;
+        }
+        // the window, from the prefetched registers
+        {
+            uint4* l16 = reinterpret_cast<uint4*>(s_in);
+#pragma unroll
+            for (int r = 0; r < S; ++r)
+                if (tid + G::kBlock * r < kW / 16) l16[tid + G::kBlock * r] = P.chunk[r];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (pos[r] != 0xFFFFFFFFu) s_q[s_bbase[pos[r] >> 16] + (pos[r] & 0xFFFFu)] = make_uint2(ex[r], ey[r]);
+        // the next fill's offsets and window: in flight during this fill's decode. Unconditional
+        // (clamped past the range end), so no register phi forces a wait on the stores below.
+        const uint32_t cur_next = cur + k;
+        {
+            const uint32_t c = min(cur_next, BB - 1);
+            prefetch_fill<G::kBlock>(P, a, tid, c, min(c + (uint32_t)kQ, BB), min(gin_next, in_end ? in_end - 1 : 0) & ~15u,
+                                     last16);
+        }
+        // the previous fill's write-back: its image is read out before this fill decodes over it
+        if (pk) flush(pcur, pk, pG0, pG1);
+        pk = k;
+        pcur = cur;
+        pG0 = gout;
+        pG1 = gout_next;
+        lds_barrier();
+        if (kMode == 3 && t_staged == 0) t_staged = __builtin_amdgcn_s_memtime();
+        if (kMode == 1) {  // diagnostic: no decode; lengths from the staged bytes keep them live
+            for (uint32_t t = tid; t < k; t += G::kBlock) {
+                const uint2 e = s_q[t];
+                s_lenst[e.y & 0xFFFu] = (e.x >> 16) + s_in[e.x & 0xFFFFu];
+            }
+        } else {
+            constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
+            Lit L = {};  // every field defined: idle lanes still run the (predicated) step
+            L.nb = 64;
+            uint32_t t = tid;
+            uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
+            bool act = false;         // lane holds a dword-path literal not yet finalised
+            uint32_t idx = 0;         // its index in the fill
+            auto begin = [&](uint32_t tt) {
+                const uint2 e = s_q[min(tt, k - 1)];
+                act = tt < k && !(e.y & kQ7Byte);
+                idx = e.y & 0xFFFu;
+                lit_begin(L, lds, e.x & 0xFFFFu, e.x >> 16);
+                L.od = (e.y >> 12) & 0x7FFFu;
+                L.oend = L.od + ((e.x >> 16) * 8u / 5u + 3u) / 4u;
+                L.live = L.live && act;
+            };
+            begin(t);
+            for (;;) {
+#pragma unroll
+                for (int s = 0; s < kRefillN; ++s) {
+                    if (kStep == 6)
+                        lit_step6<kStore>(L, lds, s_t8, s_lo, s_out);
+                    else
+                        lit_step<kStore>(L, lds, s_t8, s_lo, s_out);
+                }
+                const bool fin = t < k && !L.live;
+                if (__any(fin)) {
+                    if (fin && act) {
+                        if (kStore == kDword && L.accn) s_out32[L.od] = (uint32_t)L.acc;
+                        if (kStore == kChecked && L.accn) {
+                            if (L.od < L.oend && L.od < (uint32_t)kO / 4)
+                                s_out32[L.od] = (uint32_t)L.acc;
+                            else
+                                chk_report(2, L.od, L.oend, L.cnt);
+                        }
+                        s_lenst[idx] = L.cnt | (lit_status(L) << 24);
+                    }
+                    const bool free_lane = fin || t >= k;
+                    const uint64_t fm = __ballot(free_lane);
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+                    const uint32_t need = (uint32_t)__popcll(fm), have = qe - qb;
+                    uint32_t base = qb + rank;
+                    if (have < need) {  // wave-uniform
+                        uint32_t nb = 0;
+                        if (rank == 0 && free_lane) nb = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
+                        nb = (uint32_t)__builtin_amdgcn_readlane((int)nb, (int)__builtin_ctzll(fm));
+                        if (rank >= have) base = nb + (rank - have);
+                        qb = nb + (need - have);
+                        qe = nb + kChunk;
+                    } else {
+                        qb += need;
+                    }
+                    qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
+                    qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
+                    if (free_lane) {
+                        t = base;
+                        begin(base);
+                    }
+                }
+                if (!__any(t < k)) break;
+            }
+            // literals whose output region is unaligned / below the decoded bound: byte stores
+            // into the image with a capacity check per byte
+            for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
+                const uint2 e = s_q[tt];
+                if (e.y & kQ7Byte) {
+                    const uint32_t i = e.y & 0xFFFu;
+                    const uint32_t o = a.out_off[cur + i] + a.out_mis - ob16;
+                    Lit B = {};
+                    lit_bytes_to(B, lds, s_lo, [&](uint32_t j, uint8_t v) { s_out[o + j] = v; },
+                                 a.out_off[cur + i + 1] - a.out_off[cur + i], e.x & 0xFFFFu, e.x >> 16);
+                    s_lenst[i] = B.cnt | (lit_status(B) << 24);
+                }
+            }
+        }
+        cur = cur_next;
+        gin = gin_next;
+        gout = gout_next;
+    }
+    if (pk) {
+        lds_barrier();
+        flush(pcur, pk, pG0, pG1);
     }
     if (kMode == 3 && lane == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
