@@ -146,13 +146,13 @@ int main(int argc, char** argv) {
     CK(hipGetDeviceProperties(&prop, 0));
     const int cu = prop.multiProcessorCount;
     printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
-    run<0, 16, 126976, 4096, 4, 64, 1, 6>("v5_s6", d, ref_len, ref_st, ref_out, cu, iters);
     run7<0, 16, 45056, 86016, 2048, 4, 64, 6>("v7_s6_r4", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 4, 64, 4>("v7_s4_r4", d, ref_len, ref_st, ref_out, cu, iters);
     run7<0, 16, 45056, 86016, 2048, 3, 64, 6>("v7_s6_r3", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 6, 64, 6>("v7_s6_r6", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 8, 22528, 43008, 1024, 4, 64, 6, 2>("v7_w8x2_s6_r4", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<2, 16, 45056, 86016, 2048, 4, 64, 6>("v7_nostore", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<1, 16, 45056, 86016, 2048, 4, 64, 6>("v7_stage_flush", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 2, 64, 7>("v7_s7_r2", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 3, 64, 7>("v7_s7_r3", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 4, 64, 7>("v7_s7_r4", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 45056, 86016, 2048, 6, 64, 7>("v7_s7_r6", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<2, 16, 45056, 86016, 2048, 4, 64, 7>("v7_s7_nostore", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<1, 16, 45056, 86016, 2048, 4, 64, 7>("v7_stage_flush", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }

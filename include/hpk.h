@@ -122,6 +122,60 @@ int hpk_encode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_
 int hpk_host_register(void* ptr, size_t bytes);
 int hpk_host_unregister(void* ptr);
 
+/* ---- HPACK header blocks: two-pass decode -----------------------------------------------
+ * hpk_hdec mirrors hpack::Decoder (crates/loona-hpack/src/decoder.rs:257-555; header table
+ * crates/loona-hpack/src/lib.rs:43-289): one per connection, holding the dynamic table.
+ * hpk_hdec_decode_blocks decodes many header blocks at once — block b is
+ * blocks[block_off[b] .. block_off[b+1]) for decoder decs[b]; the blocks of one decoder must be
+ * in connection order — with every Huffman string of every block decoded in ONE batch: through
+ * `ctx` on the GPU, or, when ctx is NULL, by the library's CPU batch path
+ * (hpk_decode_batch_cpu). Per block the result equals Decoder::decode_with_cb on the same state:
+ * the headers emitted before the first error, and that error with the reference's precedence
+ * (decoder.rs:368-450). Results are returned in library-allocated buffers (hpk_blocks_out_free). */
+typedef struct hpk_hdec hpk_hdec;
+
+typedef enum hpk_block_error {   /* DecoderError (decoder.rs:237-253) and its nested kinds */
+    HPK_BLK_OK = 0,
+    HPK_BLK_HEADER_INDEX_OUT_OF_BOUNDS = 1,  /* HeaderIndexOutOfBounds                         */
+    HPK_BLK_INT_TOO_MANY_OCTETS = 2,         /* IntegerDecodingError::TooManyOctets           */
+    HPK_BLK_INT_VALUE_TOO_LARGE = 3,         /* IntegerDecodingError::ValueTooLarge (unused)  */
+    HPK_BLK_INT_NOT_ENOUGH_OCTETS = 4,       /* IntegerDecodingError::NotEnoughOctets         */
+    HPK_BLK_INT_INVALID_PREFIX = 5,          /* IntegerDecodingError::InvalidPrefix           */
+    HPK_BLK_STR_NOT_ENOUGH_OCTETS = 6,       /* StringDecodingError::NotEnoughOctets          */
+    HPK_BLK_STR_HUFFMAN = 7,                 /* StringDecodingError::HuffmanDecoderError(detail = hpk_status) */
+    HPK_BLK_INVALID_MAX_DYNAMIC_SIZE = 8,    /* InvalidMaxDynamicSize                          */
+    HPK_BLK_SIZE_UPDATE_AT_END = 9           /* SizeUpdateAtEnd                                */
+} hpk_block_error;
+
+typedef struct hpk_header {      /* one emitted (name, value), offsets into hpk_blocks_out.arena */
+    uint32_t name_off, name_len, value_off, value_len;
+} hpk_header;
+
+typedef struct hpk_block_result {
+    uint32_t first_header;       /* index into hpk_blocks_out.headers                         */
+    uint32_t n_headers;          /* headers emitted (before the error, if any)               */
+    int32_t error;               /* hpk_block_error                                           */
+    int32_t detail;              /* hpk_status for HPK_BLK_STR_HUFFMAN, else 0                 */
+} hpk_block_result;
+
+typedef struct hpk_blocks_out {
+    uint8_t* arena;
+    size_t arena_len;
+    hpk_header* headers;
+    size_t n_headers;
+    hpk_block_result* blocks;
+    uint32_t n_blocks;
+} hpk_blocks_out;
+
+hpk_hdec* hpk_hdec_create(void);                                  /* Decoder::new(): max table 4096 */
+void hpk_hdec_destroy(hpk_hdec* dec);
+int hpk_hdec_set_max_table_size(hpk_hdec* dec, size_t max_size); /* decoder.rs:296-311 */
+int hpk_hdec_set_max_allowed_table_size(hpk_hdec* dec, size_t max_allowed); /* decoder.rs:316-318 */
+int hpk_hdec_table_size(const hpk_hdec* dec, size_t* size, size_t* entries, size_t* max_size);
+int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const uint8_t* blocks, const uint32_t* block_off,
+                           uint32_t nblocks, hpk_blocks_out* out);
+void hpk_blocks_out_free(hpk_blocks_out* out);
+
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);
 

@@ -50,8 +50,31 @@ EXPORTS = (
     "hpk_encode_batch_cpu",
     "hpk_host_register",
     "hpk_host_unregister",
+    "hpk_hdec_create",
+    "hpk_hdec_destroy",
+    "hpk_hdec_set_max_table_size",
+    "hpk_hdec_set_max_allowed_table_size",
+    "hpk_hdec_table_size",
+    "hpk_hdec_decode_blocks",
+    "hpk_blocks_out_free",
     "hpk_version",
 )
+
+class Header(ctypes.Structure):
+    _fields_ = [("name_off", ctypes.c_uint32), ("name_len", ctypes.c_uint32), ("value_off", ctypes.c_uint32),
+                ("value_len", ctypes.c_uint32)]
+
+
+class BlockResult(ctypes.Structure):
+    _fields_ = [("first_header", ctypes.c_uint32), ("n_headers", ctypes.c_uint32), ("error", ctypes.c_int32),
+                ("detail", ctypes.c_int32)]
+
+
+class BlocksOut(ctypes.Structure):
+    _fields_ = [("arena", ctypes.POINTER(ctypes.c_uint8)), ("arena_len", ctypes.c_size_t),
+                ("headers", ctypes.POINTER(Header)), ("n_headers", ctypes.c_size_t),
+                ("blocks", ctypes.POINTER(BlockResult)), ("n_blocks", ctypes.c_uint32)]
+
 
 _lock = threading.Lock()
 _lib = None
@@ -108,6 +131,20 @@ def lib() -> ctypes.CDLL:
         L.hpk_host_register.restype = ctypes.c_int
         L.hpk_host_unregister.argtypes = [ctypes.c_void_p]
         L.hpk_host_unregister.restype = ctypes.c_int
+        L.hpk_hdec_create.argtypes = []
+        L.hpk_hdec_create.restype = ctypes.c_void_p
+        L.hpk_hdec_destroy.argtypes = [ctypes.c_void_p]
+        L.hpk_hdec_destroy.restype = None
+        for fn in (L.hpk_hdec_set_max_table_size, L.hpk_hdec_set_max_allowed_table_size):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+            fn.restype = ctypes.c_int
+        L.hpk_hdec_table_size.argtypes = [ctypes.c_void_p, c_sizep, c_sizep, c_sizep]
+        L.hpk_hdec_table_size.restype = ctypes.c_int
+        L.hpk_hdec_decode_blocks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint32, ctypes.POINTER(BlocksOut)]
+        L.hpk_hdec_decode_blocks.restype = ctypes.c_int
+        L.hpk_blocks_out_free.argtypes = [ctypes.POINTER(BlocksOut)]
+        L.hpk_blocks_out_free.restype = None
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

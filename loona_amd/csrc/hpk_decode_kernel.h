@@ -44,6 +44,7 @@ struct Lit {
     uint32_t ocap;  // output capacity (byte stores only)
     uint32_t oend;  // diagnostic mode 4: one past the last output dword of the literal
     bool live;      // still decoding
+    bool park;      // step 7: waiting at the next refill point for a leading-ones lookup
 };
 
 enum StoreMode { kDword = 0, kNoStore = 1, kChecked = 3 };
@@ -274,6 +275,73 @@ __device__ __forceinline__ void lit_step6(Lit& L, const Src& src, const uint8_t*
             lit_emit_g<kStore>(L, s1, 1u, out8);
             L.live = L.rem != 0u;
         }
+    }
+}
+
+// v7 step: lit_step6 without the in-step branch. A lane whose next code is longer than 8 bits
+// (~0.8 % of header-value codes, but with 64 lanes x ~3.5 codes per step ~80 % of wave-steps
+// saw one) parks and idles until the wave's next refill point, where all parked lanes take
+// their leading-ones lookup together (lit_unpark): one branch per kRefillN steps.
+template <int kStore, class Src>
+__device__ __forceinline__ void lit_step7(Lit& L, const Src& src, const uint8_t* __restrict__ t8,
+                                          uint8_t* __restrict__ out8) {
+    lit_refill(L, src);
+    constexpr uint32_t M = (1u << 10) | (1u << 23) | (1u << 31);
+    const uint32_t hi = (uint32_t)(L.win >> 32);
+    const uint32_t nh = ~hi;
+    uint32_t f[5], sym[4];
+    bool fast[4], fits[4];
+    f[0] = 27;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = __builtin_amdgcn_ubfe(nh << (5 * i), f[i], 5);  // 31 - t_i
+        f[i + 1] = f[i] - (uint32_t)__builtin_popcount(M << s);
+        const uint32_t b = __builtin_amdgcn_ubfe(hi, f[i] - (3 + 5 * i), 8);
+        fast[i] = b < 0xFEu;
+        sym[i] = t8[b];
+        fits[i] = f[i + 1] + L.rem >= 32u + 5u * i;
+    }
+    const bool run = L.live && !L.park;
+    const bool m0 = run && fast[0] && fits[0];
+    const bool m1 = m0 && fast[1] && fits[1];
+    const bool m2 = m1 && fast[2] && fits[2];
+    const bool m3 = m2 && fast[3] && fits[3];
+    const uint32_t g = (uint32_t)m0 + (uint32_t)m1 + (uint32_t)m2 + (uint32_t)m3;
+    const uint32_t fg = m3 ? f[4] : m2 ? f[3] : m1 ? f[2] : m0 ? f[1] : 27u;
+    const uint32_t use = 5u * g + 27u - fg;
+    // the first invalid code is a long one (park) or runs past the literal (only padding left)
+    const bool bad_fast = (m2 && fast[3]) || (m1 && !m2 && fast[2]) || (m0 && !m1 && fast[1]) || (!m0 && fast[0]);
+    const bool park = run && !m3 && !bad_fast;
+    L.win <<= use;
+    L.nb -= use;
+    L.rem -= use;
+    const uint32_t packed = sym[0] | (sym[1] << 8) | (sym[2] << 16) | (sym[3] << 24);
+    lit_emit_g<kStore>(L, packed, g, out8);
+    L.live = run ? (park || (m3 && L.rem != 0u)) : L.live;
+    L.park = L.park || park;
+}
+
+// The parked lanes' long code: one lookup in the leading-ones table.
+template <int kStore, class Src>
+__device__ __forceinline__ void lit_unpark(Lit& L, const Src& src, const uint16_t* __restrict__ lo,
+                                           uint8_t* __restrict__ out8) {
+    L.park = false;
+    lit_refill(L, src);
+    const uint32_t w = (uint32_t)(L.win >> 32);
+    uint32_t s1, len;
+    bool eos;
+    lo_decode(w, lo, s1, len, eos);
+    if (len > L.rem) {
+        L.live = false;  // only padding left
+    } else if (eos) {
+        L.st = HPK_EOS_IN_STRING;  // huffman.rs:112-116
+        L.live = false;
+    } else {
+        L.win <<= len;
+        L.nb -= len;
+        L.rem -= len;
+        lit_emit_g<kStore>(L, s1, 1u, out8);
+        L.live = L.rem != 0u;
     }
 }
 
@@ -858,10 +926,15 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
             for (;;) {
 #pragma unroll
                 for (int s = 0; s < kRefillN; ++s) {
-                    if (kStep == 6)
+                    if (kStep == 7)
+                        lit_step7<kStore>(L, lds, s_t8, s_out);
+                    else if (kStep == 6)
                         lit_step6<kStore>(L, lds, s_t8, s_lo, s_out);
                     else
                         lit_step<kStore>(L, lds, s_t8, s_lo, s_out);
+                }
+                if (kStep == 7 && __any(L.park)) {
+                    if (L.park) lit_unpark<kStore>(L, lds, s_lo, s_out);
                 }
                 const bool fin = t < k && !L.live;
                 if (__any(fin)) {

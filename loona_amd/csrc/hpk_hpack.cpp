@@ -1,0 +1,444 @@
+// hpk_hpack.cpp — two-pass HPACK header-block decoding around the batched Huffman kernel
+// (SURVEY §8f-1). Host code: the C ABI's hpk_hdec_* entry points (include/hpk.h).
+//
+// Reference: hpack::Decoder, crates/loona-hpack/src/decoder.rs:257-555, with its header table
+// (crates/loona-hpack/src/lib.rs:43-289). Huffman results never depend on dynamic-table state,
+// so the work splits in three:
+//   1. scan (per block): walk the field representations (decoder.rs:368-450) with decode_integer
+//      (decoder.rs:67-125) and the string framing of decode_string (decoder.rs:135-163): record
+//      every field and the byte span of every string; stop at the first integer / length error;
+//   2. one Huffman batch for the H-bit strings of ALL blocks (device: hpk_decode_batch through a
+//      context; or the library's CPU batch path when the caller passes no context);
+//   3. apply (per block, in order per decoder): table lookups, insertions, size updates and the
+//      emitted header list, reporting the FIRST error in field order exactly as the reference's
+//      single pass would (index integer, then name string or name index, then value string;
+//      Huffman status of a string where the reference would have decoded it).
+#include <stdlib.h>
+#include <string.h>
+
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/hpk.h"
+
+namespace {
+
+// RFC 7541 Appendix A (the reference keeps it as STATIC_TABLE, crates/loona-hpack/src/lib.rs).
+const char* const kStatic[61][2] = {
+    {":authority", ""},
+    {":method", "GET"},
+    {":method", "POST"},
+    {":path", "/"},
+    {":path", "/index.html"},
+    {":scheme", "http"},
+    {":scheme", "https"},
+    {":status", "200"},
+    {":status", "204"},
+    {":status", "206"},
+    {":status", "304"},
+    {":status", "400"},
+    {":status", "404"},
+    {":status", "500"},
+    {"accept-charset", ""},
+    {"accept-encoding", "gzip, deflate"},
+    {"accept-language", ""},
+    {"accept-ranges", ""},
+    {"accept", ""},
+    {"access-control-allow-origin", ""},
+    {"age", ""},
+    {"allow", ""},
+    {"authorization", ""},
+    {"cache-control", ""},
+    {"content-disposition", ""},
+    {"content-encoding", ""},
+    {"content-language", ""},
+    {"content-length", ""},
+    {"content-location", ""},
+    {"content-range", ""},
+    {"content-type", ""},
+    {"cookie", ""},
+    {"date", ""},
+    {"etag", ""},
+    {"expect", ""},
+    {"expires", ""},
+    {"from", ""},
+    {"host", ""},
+    {"if-match", ""},
+    {"if-modified-since", ""},
+    {"if-none-match", ""},
+    {"if-range", ""},
+    {"if-unmodified-since", ""},
+    {"last-modified", ""},
+    {"link", ""},
+    {"location", ""},
+    {"max-forwards", ""},
+    {"proxy-authenticate", ""},
+    {"proxy-authorization", ""},
+    {"range", ""},
+    {"referer", ""},
+    {"refresh", ""},
+    {"retry-after", ""},
+    {"server", ""},
+    {"set-cookie", ""},
+    {"strict-transport-security", ""},
+    {"transfer-encoding", ""},
+    {"user-agent", ""},
+    {"vary", ""},
+    {"via", ""},
+    {"www-authenticate", ""},
+};
+
+// decode_integer (decoder.rs:67-125): prefix 1..8, at most 5 octets.
+int decode_integer(const uint8_t* p, size_t n, int prefix, uint64_t* value, size_t* consumed) {
+    if (prefix < 1 || prefix > 8) return HPK_BLK_INT_INVALID_PREFIX;
+    if (n == 0) return HPK_BLK_INT_NOT_ENOUGH_OCTETS;
+    const uint32_t mask = prefix == 8 ? 0xFFu : ((1u << prefix) - 1u);
+    uint64_t v = p[0] & mask;
+    if (v < mask) {
+        *value = v;
+        *consumed = 1;
+        return HPK_BLK_OK;
+    }
+    size_t total = 1;
+    unsigned m = 0;
+    for (size_t i = 1; i < n; ++i) {
+        const uint8_t b = p[i];
+        total += 1;
+        v += (uint64_t)(b & 127u) << m;
+        m += 7;
+        if (!(b & 128u)) {
+            *value = v;
+            *consumed = total;
+            return HPK_BLK_OK;
+        }
+        if (total == 5) return HPK_BLK_INT_TOO_MANY_OCTETS;
+    }
+    return HPK_BLK_INT_NOT_ENOUGH_OCTETS;
+}
+
+struct Str {
+    uint32_t off = 0;  // absolute offset of the string bytes in the blocks buffer
+    uint32_t len = 0;
+    bool huff = false;
+    uint32_t lit = 0;  // index in the Huffman batch (huff only)
+};
+
+enum Kind : uint8_t { kIndexed, kLitIncr, kSizeUpdate, kLitNever, kLitPlain };
+
+// Stages of one field in the reference's order; a scan error is recorded with the stage at which
+// the reference would have raised it.
+enum Stage : uint8_t { kStIndex = 0, kStName = 1, kStValue = 2 };
+
+struct Field {
+    Kind kind;
+    uint64_t index = 0;  // header index / name index / new table size
+    Str name, value;
+    int err = HPK_BLK_OK;  // scan error in this field (the last field scanned)
+    Stage err_stage = kStIndex;
+};
+
+struct Scan {
+    std::vector<Field> fields;
+};
+
+// decode_string's framing (decoder.rs:135-163) without the Huffman step.
+int scan_string(const uint8_t* base, size_t pos, size_t end, Str* s, size_t* consumed) {
+    uint64_t len;
+    size_t c;
+    int e = decode_integer(base + pos, end - pos, 7, &len, &c);
+    if (e) return e;
+    if (c + len > end - pos) return HPK_BLK_STR_NOT_ENOUGH_OCTETS;
+    s->off = (uint32_t)(pos + c);
+    s->len = (uint32_t)len;
+    s->huff = (base[pos] & 128u) != 0;
+    *consumed = c + (size_t)len;
+    return HPK_BLK_OK;
+}
+
+void scan_block(const uint8_t* base, size_t begin, size_t end, Scan* out, std::vector<uint32_t>* hoff,
+                std::vector<uint32_t>* hlen) {
+    size_t pos = begin;
+    auto add_huff = [&](Str& s) {
+        if (!s.huff) return;
+        s.lit = (uint32_t)hoff->size();
+        hoff->push_back(s.off);
+        hlen->push_back(s.len);
+    };
+    while (pos < end) {
+        Field f;
+        const uint8_t b = base[pos];
+        f.kind = (b & 128u) ? kIndexed : (b & 64u) ? kLitIncr : (b & 32u) ? kSizeUpdate : (b & 16u) ? kLitNever : kLitPlain;
+        size_t c = 0;
+        if (f.kind == kIndexed || f.kind == kSizeUpdate) {
+            f.err = decode_integer(base + pos, end - pos, f.kind == kIndexed ? 7 : 5, &f.index, &c);
+            out->fields.push_back(f);
+            if (f.err) return;
+            pos += c;
+            continue;
+        }
+        // decode_literal (decoder.rs:502-527)
+        const int prefix = f.kind == kLitIncr ? 6 : 4;
+        f.err = decode_integer(base + pos, end - pos, prefix, &f.index, &c);
+        if (f.err) {
+            out->fields.push_back(f);
+            return;
+        }
+        size_t at = pos + c;
+        if (f.index == 0) {
+            size_t cn;
+            f.err = scan_string(base, at, end, &f.name, &cn);
+            if (f.err) {
+                f.err_stage = kStName;
+                out->fields.push_back(f);
+                return;
+            }
+            add_huff(f.name);
+            at += cn;
+        }
+        size_t cv;
+        f.err = scan_string(base, at, end, &f.value, &cv);
+        if (f.err) {
+            f.err_stage = kStValue;
+            out->fields.push_back(f);
+            return;
+        }
+        add_huff(f.value);
+        at += cv;
+        out->fields.push_back(f);
+        pos = at;
+    }
+}
+
+}  // namespace
+
+// Decoder state: the dynamic table (lib.rs:43-164) and the SizeUpdate limit (decoder.rs:316-318).
+struct hpk_hdec {
+    std::deque<std::pair<std::string, std::string>> table;  // front = newest
+    size_t size = 0;
+    size_t max_size = 4096;
+    bool has_max_allowed = false;
+    size_t max_allowed = 0;
+
+    void consolidate() {
+        while (size > max_size) {
+            const auto& last = table.back();
+            size -= last.first.size() + last.second.size() + 32;
+            table.pop_back();
+        }
+    }
+    void add(std::string n, std::string v) {
+        size += n.size() + v.size() + 32;
+        table.emplace_front(std::move(n), std::move(v));
+        consolidate();
+    }
+    // HeaderTable::get_from_table (lib.rs:228-255): 1-based, static then dynamic
+    bool get(uint64_t index, const char** n, size_t* nl, const char** v, size_t* vl) const {
+        if (index == 0) return false;
+        const uint64_t ri = index - 1;
+        if (ri < 61) {
+            *n = kStatic[ri][0];
+            *nl = strlen(*n);
+            *v = kStatic[ri][1];
+            *vl = strlen(*v);
+            return true;
+        }
+        const uint64_t di = ri - 61;
+        if (di >= table.size()) return false;
+        const auto& e = table[(size_t)di];
+        *n = e.first.data();
+        *nl = e.first.size();
+        *v = e.second.data();
+        *vl = e.second.size();
+        return true;
+    }
+};
+
+extern "C" hpk_hdec* hpk_hdec_create(void) { return new (std::nothrow) hpk_hdec(); }
+
+extern "C" void hpk_hdec_destroy(hpk_hdec* d) { delete d; }
+
+extern "C" int hpk_hdec_set_max_table_size(hpk_hdec* d, size_t n) {
+    if (!d) return HPK_E_INVAL;
+    if (d->has_max_allowed && n > d->max_allowed) return HPK_E_INVAL;  // the reference asserts
+    d->max_size = n;
+    d->consolidate();
+    return HPK_E_OK;
+}
+
+extern "C" int hpk_hdec_set_max_allowed_table_size(hpk_hdec* d, size_t n) {
+    if (!d) return HPK_E_INVAL;
+    d->has_max_allowed = true;
+    d->max_allowed = n;
+    return HPK_E_OK;
+}
+
+extern "C" int hpk_hdec_table_size(const hpk_hdec* d, size_t* size, size_t* entries, size_t* max_size) {
+    if (!d) return HPK_E_INVAL;
+    if (size) *size = d->size;
+    if (entries) *entries = d->table.size();
+    if (max_size) *max_size = d->max_size;
+    return HPK_E_OK;
+}
+
+namespace {
+
+struct Out {
+    std::vector<uint8_t> arena;
+    std::vector<hpk_header> headers;
+};
+
+uint32_t put(Out& o, const void* p, size_t n) {
+    const uint32_t at = (uint32_t)o.arena.size();
+    o.arena.insert(o.arena.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+    return at;
+}
+
+struct Huff {
+    const std::vector<uint8_t>* out;
+    const std::vector<uint32_t>* oo;
+    const std::vector<uint32_t>* len;
+    const std::vector<uint8_t>* st;
+};
+
+// Pass 3 for one block: the reference's single pass over the scanned fields.
+void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const Huff& h, Out& o, hpk_block_result* r) {
+    r->first_header = (uint32_t)o.headers.size();
+    r->n_headers = 0;
+    r->error = HPK_BLK_OK;
+    r->detail = 0;
+    auto fail = [&](int e, int detail) {
+        r->error = e;
+        r->detail = detail;
+    };
+    // string bytes: raw from the block, Huffman from the batch (status checked by the caller)
+    auto str = [&](const Str& s, const uint8_t** p, size_t* n) {
+        if (s.huff) {
+            *p = h.out->data() + (*h.oo)[s.lit];
+            *n = (*h.len)[s.lit];
+        } else {
+            *p = base + s.off;
+            *n = s.len;
+        }
+    };
+    auto huff_err = [&](const Str& s) -> int { return s.huff ? (*h.st)[s.lit] : 0; };
+    bool last_was_size_update = false;
+    for (size_t fi = 0; fi < sc.fields.size(); ++fi) {
+        const Field& f = sc.fields[fi];
+        last_was_size_update = f.kind == kSizeUpdate;
+        if (f.err && f.err_stage == kStIndex) return fail(f.err, 0);
+        if (f.kind == kIndexed) {
+            const char *n, *v;
+            size_t nl, vl;
+            if (!d->get(f.index, &n, &nl, &v, &vl)) return fail(HPK_BLK_HEADER_INDEX_OUT_OF_BOUNDS, 0);
+            hpk_header hd;
+            hd.name_len = (uint32_t)nl;
+            hd.name_off = put(o, n, nl);
+            hd.value_len = (uint32_t)vl;
+            hd.value_off = put(o, v, vl);
+            o.headers.push_back(hd);
+            r->n_headers += 1;
+            continue;
+        }
+        if (f.kind == kSizeUpdate) {  // update_max_dynamic_size (decoder.rs:538-554)
+            if (d->has_max_allowed && f.index > d->max_allowed) return fail(HPK_BLK_INVALID_MAX_DYNAMIC_SIZE, 0);
+            d->max_size = (size_t)f.index;
+            d->consolidate();
+            continue;
+        }
+        // literal: name (literal string or table name), then value
+        const uint8_t* np;
+        size_t nl;
+        std::string name_store;
+        if (f.index == 0) {
+            if (f.err && f.err_stage == kStName) return fail(f.err, 0);
+            if (int hs = huff_err(f.name)) return fail(HPK_BLK_STR_HUFFMAN, hs);
+            str(f.name, &np, &nl);
+        } else {
+            const char *n, *v;
+            size_t vl;
+            if (!d->get(f.index, &n, &nl, &v, &vl)) return fail(HPK_BLK_HEADER_INDEX_OUT_OF_BOUNDS, 0);
+            name_store.assign(n, nl);  // the insertion below may evict the entry it points into
+            np = (const uint8_t*)name_store.data();
+        }
+        if (f.err && f.err_stage == kStValue) return fail(f.err, 0);
+        if (int hs = huff_err(f.value)) return fail(HPK_BLK_STR_HUFFMAN, hs);
+        const uint8_t* vp;
+        size_t vl;
+        str(f.value, &vp, &vl);
+        hpk_header hd;
+        hd.name_len = (uint32_t)nl;
+        hd.name_off = put(o, np, nl);
+        hd.value_len = (uint32_t)vl;
+        hd.value_off = put(o, vp, vl);
+        o.headers.push_back(hd);
+        r->n_headers += 1;
+        if (f.kind == kLitIncr) d->add(std::string((const char*)np, nl), std::string((const char*)vp, vl));
+    }
+    if (last_was_size_update) fail(HPK_BLK_SIZE_UPDATE_AT_END, 0);
+}
+
+}  // namespace
+
+extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const uint8_t* blocks,
+                                      const uint32_t* block_off, uint32_t nblocks, hpk_blocks_out* out) {
+    if (!decs || !block_off || !out || (nblocks && block_off[nblocks] && !blocks)) return HPK_E_INVAL;
+    memset(out, 0, sizeof *out);
+    for (uint32_t b = 0; b < nblocks; ++b)
+        if (!decs[b] || block_off[b + 1] < block_off[b]) return HPK_E_INVAL;
+    // pass 1: scan every block, gather the Huffman strings
+    std::vector<Scan> scans(nblocks);
+    std::vector<uint32_t> hoff, hlen;
+    for (uint32_t b = 0; b < nblocks; ++b) scan_block(blocks, block_off[b], block_off[b + 1], &scans[b], &hoff, &hlen);
+    // pass 2: one batch for all of them
+    const uint32_t n = (uint32_t)hoff.size();
+    std::vector<uint32_t> in_off(n + 1), out_off(n + 1), len(n ? n : 1);
+    std::vector<uint8_t> st(n ? n : 1);
+    size_t tot = 0, otot = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        in_off[i] = (uint32_t)tot;
+        out_off[i] = (uint32_t)otot;
+        tot += hlen[i];
+        otot += ((hpk_decoded_bound(hlen[i]) + 3) & ~(size_t)3);
+        if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
+    }
+    in_off[n] = (uint32_t)tot;
+    out_off[n] = (uint32_t)otot;
+    std::vector<uint8_t> in(tot ? tot : 1), dec(otot ? otot : 1);
+    for (uint32_t i = 0; i < n; ++i) memcpy(in.data() + in_off[i], blocks + hoff[i], hlen[i]);
+    if (n) {
+        const int rc = ctx ? hpk_decode_batch(ctx, in.data(), in_off.data(), n, dec.data(), out_off.data(), len.data(),
+                                              st.data(), HPK_PTR_HOST)
+                           : hpk_decode_batch_cpu(in.data(), in_off.data(), n, dec.data(), out_off.data(), len.data(),
+                                                  st.data(), 0);
+        if (rc) return rc;
+    }
+    // pass 3: apply in block order (the blocks of one decoder are in connection order)
+    Out o;
+    std::vector<hpk_block_result> res(nblocks);
+    const Huff h{&dec, &out_off, &len, &st};
+    for (uint32_t b = 0; b < nblocks; ++b) apply_block(decs[b], blocks, scans[b], h, o, &res[b]);
+    // hand the results over in malloc'd buffers (hpk_blocks_out_free)
+    out->arena_len = o.arena.size();
+    out->n_headers = o.headers.size();
+    out->n_blocks = nblocks;
+    out->arena = (uint8_t*)malloc(o.arena.size() ? o.arena.size() : 1);
+    out->headers = (hpk_header*)malloc((o.headers.size() ? o.headers.size() : 1) * sizeof(hpk_header));
+    out->blocks = (hpk_block_result*)malloc((nblocks ? nblocks : 1) * sizeof(hpk_block_result));
+    if (!out->arena || !out->headers || !out->blocks) {
+        hpk_blocks_out_free(out);
+        return HPK_E_INVAL;
+    }
+    if (!o.arena.empty()) memcpy(out->arena, o.arena.data(), o.arena.size());
+    if (!o.headers.empty()) memcpy(out->headers, o.headers.data(), o.headers.size() * sizeof(hpk_header));
+    if (nblocks) memcpy(out->blocks, res.data(), nblocks * sizeof(hpk_block_result));
+    return HPK_E_OK;
+}
+
+extern "C" void hpk_blocks_out_free(hpk_blocks_out* out) {
+    if (!out) return;
+    free(out->arena);
+    free(out->headers);
+    free(out->blocks);
+    memset(out, 0, sizeof *out);
+}

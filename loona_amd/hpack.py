@@ -1,0 +1,149 @@
+"""HPACK header-block decoding with batched Huffman strings.
+
+Mirrors loona-hpack's `hpack::Decoder` (crates/loona-hpack/src/decoder.rs:257-555):
+
+    d = Decoder()                       # Decoder::new(), dynamic table max 4096
+    d.set_max_table_size(256)           # decoder.rs:296-311
+    d.set_max_allowed_table_size(4096)  # decoder.rs:316-318
+    headers = d.decode(block)           # list[(name, value)] or raises DecoderError
+
+and adds the batched form the GPU is for:
+
+    decode_blocks([(d1, block_a), (d2, block_b), (d1, block_c)], codec)
+
+which decodes every Huffman string of every block in one hpk_decode_batch on `codec`'s device
+(or with the library's CPU batch path when codec is None) and then applies each block to its
+decoder in order. Error values carry the reference's enum names:
+    DecoderError("HeaderIndexOutOfBounds")
+    DecoderError("IntegerDecodingError", "TooManyOctets" | "NotEnoughOctets" | ...)
+    DecoderError("StringDecodingError", "NotEnoughOctets")
+    DecoderError("StringDecodingError", ("HuffmanDecoderError", status))
+    DecoderError("InvalidMaxDynamicSize"), DecoderError("SizeUpdateAtEnd")
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+_ERR = {
+    1: ("HeaderIndexOutOfBounds", None),
+    2: ("IntegerDecodingError", "TooManyOctets"),
+    3: ("IntegerDecodingError", "ValueTooLarge"),
+    4: ("IntegerDecodingError", "NotEnoughOctets"),
+    5: ("IntegerDecodingError", "InvalidPrefix"),
+    6: ("StringDecodingError", "NotEnoughOctets"),
+    8: ("InvalidMaxDynamicSize", None),
+    9: ("SizeUpdateAtEnd", None),
+}
+
+_DISPLAY = {
+    "HeaderIndexOutOfBounds": "Header index out of bounds",
+    "InvalidMaxDynamicSize": "Dynamic table size exceeds the maximum size",
+    "SizeUpdateAtEnd": "Dynamic table size update at the end of a header block",
+}
+
+
+class DecoderError(Exception):
+    """DecoderError (decoder.rs:237-253): .kind = variant name, .detail = nested kind."""
+
+    def __init__(self, kind, detail=None):
+        super().__init__(_DISPLAY.get(kind, kind if detail is None else f"{kind}: {detail}"))
+        self.kind = kind
+        self.detail = detail
+
+    def __eq__(self, other):
+        return isinstance(other, DecoderError) and (self.kind, self.detail) == (other.kind, other.detail)
+
+    def __hash__(self):
+        return hash((self.kind, self.detail))
+
+
+def _error(code, detail):
+    if code == 7:
+        return DecoderError("StringDecodingError", ("HuffmanDecoderError", int(detail)))
+    kind, det = _ERR[code]
+    return DecoderError(kind, det)
+
+
+class Decoder:
+    """hpack::Decoder: one per connection (holds the dynamic table)."""
+
+    def __init__(self):
+        self._L = _lib.lib()
+        self._h = self._L.hpk_hdec_create()
+        if not self._h:
+            raise MemoryError("hpk_hdec_create")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._L.hpk_hdec_destroy(h)
+
+    def set_max_table_size(self, n: int):
+        if self._L.hpk_hdec_set_max_table_size(self._h, n) != 0:
+            raise AssertionError(f"new_max_size ({n}) > max_allowed_size")  # the reference asserts
+
+    def set_max_allowed_table_size(self, n: int):
+        _lib.check(self._L.hpk_hdec_set_max_allowed_table_size(self._h, n), "hpk_hdec_set_max_allowed_table_size")
+
+    def table_size(self):
+        """(size in octets per RFC 7541 §4.1, entries, max size)."""
+        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        self._L.hpk_hdec_table_size(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def decode_with_cb(self, buf: bytes, cb, codec=None):
+        """decoder.rs:368-450: cb(name, value) for each header; raises the first error."""
+        (res,) = _decode_raw([(self, buf)], codec)
+        headers, err = res
+        for n, v in headers:
+            cb(n, v)
+        if err is not None:
+            raise err
+
+    def decode(self, buf: bytes, codec=None):
+        """decoder.rs:461-469: the header list, or DecoderError."""
+        (res,) = _decode_raw([(self, buf)], codec)
+        headers, err = res
+        if err is not None:
+            raise err
+        return headers
+
+
+def _decode_raw(pairs, codec):
+    L = _lib.lib()
+    n = len(pairs)
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum([len(b) for _, b in pairs], out=off[1:])
+    if off[-1] >= 2**32:
+        raise ValueError("header blocks of one call must stay below 4 GiB")
+    blob = np.frombuffer(b"".join(bytes(b) for _, b in pairs) or b"\0", dtype=np.uint8).copy()
+    off32 = off.astype(np.uint32)
+    decs = (ctypes.c_void_p * max(n, 1))(*[d._h for d, _ in pairs])
+    out = _lib.BlocksOut()
+    ctx = codec._h if codec is not None else None
+    rc = L.hpk_hdec_decode_blocks(ctx, decs, blob.ctypes.data, off32.ctypes.data, n, ctypes.byref(out))
+    _lib.check(rc, "hpk_hdec_decode_blocks")
+    try:
+        arena = ctypes.string_at(out.arena, out.arena_len) if out.arena_len else b""
+        res = []
+        for b in range(n):
+            r = out.blocks[b]
+            hs = []
+            for j in range(r.first_header, r.first_header + r.n_headers):
+                h = out.headers[j]
+                hs.append((arena[h.name_off : h.name_off + h.name_len], arena[h.value_off : h.value_off + h.value_len]))
+            res.append((hs, None if r.error == 0 else _error(r.error, r.detail)))
+        return res
+    finally:
+        L.hpk_blocks_out_free(ctypes.byref(out))
+
+
+def decode_blocks(pairs, codec=None):
+    """[(Decoder, block bytes)] -> [header list | DecoderError], all Huffman strings in one batch.
+    The blocks of one decoder are applied in list order (connection order)."""
+    return [hs if err is None else err for hs, err in _decode_raw(pairs, codec)]

@@ -207,3 +207,36 @@ def test_host_pointer_mode_pipelined(codec):
     e = codec.encode_host(w.dec_blob, w.dec_off)
     assert not e[3].any()
     assert np.array_equal(e[2].astype(np.int64), np.diff(w.enc_off.astype(np.int64)))
+
+
+def test_hpack_blocks_on_device(codec):
+    """Two-pass HPACK block decoding with the Huffman batch on the GPU: every interop story in one
+    call (one decoder per story) and seeded corruptions vs the decoder.rs restatement."""
+    import random
+
+    from hpk_util import hpack_ref
+
+    from loona_amd import hpack
+
+    inter = load("interop.json.gz")
+    pairs, want = [], []
+    for enc in sorted(inter):
+        for story in inter[enc]:
+            d = hpack.Decoder()
+            for c in story["cases"]:
+                pairs.append((d, bytes.fromhex(c["wire"])))
+                want.append([(n.encode(), v.encode()) for n, v in c["headers"]])
+    assert hpack.decode_blocks(pairs, codec) == want
+    rng = random.Random(3)
+    pairs, want = [], []
+    for _ in range(2000):
+        w = bytearray(bytes.fromhex(rng.choice(rng.choice(inter[rng.choice(sorted(inter))])["cases"])["wire"]))
+        if w:
+            w[rng.randrange(len(w))] ^= 1 << rng.randrange(8)
+        pairs.append((hpack.Decoder(), bytes(w)))
+        r = hpack_ref.Decoder()
+        try:
+            want.append(r.decode(bytes(w)))
+        except hpack_ref.DecoderError as e:
+            want.append(hpack.DecoderError(e.kind, e.detail))
+    assert hpack.decode_blocks(pairs, codec) == want
