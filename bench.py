@@ -11,7 +11,7 @@ Multi-GPU (`--gpus N` under torch.distributed.run): weak scaling, each rank deco
 bytes / max time.
 
 Extras on the JSON line:
-  roofline      dominant kernel (hpk_decode_kernel): algorithmic bytes per launch
+  roofline      dominant kernel (hpk_decode7): algorithmic bytes per launch
                 (sum of enc + dec + 13 per literal) / average launch time, against
                 the 8.0 TB/s HBM3E spec peak; traffic = PMC HBM bytes per launch from the
                 committed rocprofv3 counter summary (profiles/), null when absent
@@ -203,7 +203,8 @@ def main():
             try:
                 with open(args.pmc) as f:
                     pm = json.load(f)
-                if pm.get("literals") == n:
+                # only a summary of this exact kernel build on this workload counts
+                if pm.get("literals") == n and pm.get("kernel_version") == _lib.lib().hpk_version().decode():
                     traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -239,7 +240,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "hpk_decode_kernel",
+                "kernel": "hpk_decode7",
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
             },

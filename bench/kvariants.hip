@@ -34,7 +34,7 @@ template <int kMode, class Fn>
 static void run_fn(const char* name, Fn fn, int lds, int block, int blocks_per_cu, Dev& d,
                    const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                    const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    if (lds) CK(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     dim3 grid(num_cu * blocks_per_cu), blk(block);
     CK(hipMemset(d.a.out_len, 0xFF, d.n * 4));
     CK(hipMemset(d.a.out_base, 0xAB, d.out_bytes));
@@ -60,11 +60,13 @@ static void run_fn(const char* name, Fn fn, int lds, int block, int blocks_per_c
     std::vector<uint32_t> oo(d.n + 1);
     CK(hipMemcpy(oo.data(), d.a.out_off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
     size_t badb = 0;
-    if (kMode == 0)
+    if (kMode == 0 || kMode == 4)
         for (uint32_t i = 0; i < d.n; ++i)
             if (memcmp(&out[oo[i]], &ref_out[oo[i]], ref_len[i]) != 0) ++badb;
-    printf("{\"variant\": \"%s\", \"us\": %.2f, \"bad_len_status\": %zu, \"bad_bytes\": %zu}\n", name,
-           ms * 1000.0 / iters, bad, badb);
+    unsigned long long chk[8] = {0};
+    if (kMode == 4) CK(hipMemcpyFromSymbol(chk, HIP_SYMBOL(g_chk), sizeof chk));
+    printf("{\"variant\": \"%s\", \"us\": %.2f, \"bad_len_status\": %zu, \"bad_bytes\": %zu, \"chk\": [%llu, %llu, %llu, %llu]}\n",
+           name, ms * 1000.0 / iters, bad, badb, chk[0], chk[1], chk[2], chk[3]);
     fflush(stdout);
 }
 
@@ -81,8 +83,8 @@ static void run(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, 
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kR, int kC, int kStep, int kBlocksPerCu = 1>
 static void run7(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                  const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
-    using G = Geo7<kWaves, kW, kO, kQ>;
-    run_fn<kMode>(name, hpk_decode7<kMode, kWaves, kW, kO, kQ, kR, kC, kStep>, G::kLdsBytes, G::kBlock, kBlocksPerCu,
+    using G = Geo7<kWaves, kW, kO, kQ, (kStep >= 8)>;
+    run_fn<kMode>(name, hpk_decode7<kMode, kWaves, kW, kO, kQ, kR, kC, kStep>, 0, G::kBlock, kBlocksPerCu,
                   d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
@@ -114,7 +116,7 @@ int main(int argc, char** argv) {
     d.n = n;
     d.out_bytes = ob;
     uint8_t *d_in, *d_out, *d_st;
-    uint32_t *d_io, *d_oo, *d_len, *d_lut;
+    uint32_t *d_io, *d_oo, *d_len, *d_lut, *d_lut2;
     uint16_t* d_lo;
     CK(hipMalloc(&d_in, eb + 64));
     CK(hipMalloc(&d_out, ob));
@@ -124,6 +126,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_len, n * 4));
     CK(hipMalloc(&d_lut, sizeof(tab.t8)));
     CK(hipMalloc(&d_lo, sizeof(tab.lo)));
+    CK(hipMalloc(&d_lut2, sizeof(tab.lut)));
+    CK(hipMemcpy(d_lut2, tab.lut, sizeof(tab.lut), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_in, blob.data(), eb, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_io, in_off.data(), (n + 1) * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_oo, out_off.data(), (n + 1) * 4, hipMemcpyHostToDevice));
@@ -141,18 +145,18 @@ int main(int argc, char** argv) {
     a.status = d_st;
     a.t8 = reinterpret_cast<const uint8_t*>(d_lut);
     a.lo = d_lo;
+    a.lut = d_lut2;
     a.dbg = nullptr;
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int cu = prop.multiProcessorCount;
     printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
-    run7<0, 16, 45056, 86016, 2048, 4, 64, 6>("v7_s6_r4", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 3, 64, 6>("v7_s6_r3", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 2, 64, 7>("v7_s7_r2", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 3, 64, 7>("v7_s7_r3", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 4, 64, 7>("v7_s7_r4", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 45056, 86016, 2048, 6, 64, 7>("v7_s7_r6", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<2, 16, 45056, 86016, 2048, 4, 64, 7>("v7_s7_nostore", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<1, 16, 45056, 86016, 2048, 4, 64, 7>("v7_stage_flush", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 40960, 79104, 2048, 6, 64, 8>("v8_r6", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<4, 16, 40960, 79104, 2048, 4, 128, 10>("v10_r4_checked", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 40960, 79104, 2048, 3, 128, 10>("v10_r3", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 40960, 79104, 2048, 4, 128, 10>("v10_r4", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<0, 16, 40960, 79104, 2048, 6, 128, 10>("v10_r6", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<2, 16, 40960, 79104, 2048, 4, 128, 10>("v10_r4_nostore", d, ref_len, ref_st, ref_out, cu, iters);
+    run7<1, 16, 40960, 79104, 2048, 4, 128, 10>("v10_stage", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }

@@ -5,39 +5,38 @@
 // (crates/loona-hpack/src/huffman.rs:95-161), with identical results per literal: decoded bytes,
 // and status Ok / PaddingTooLarge / InvalidPadding / EOSInString with the reference's precedence.
 //
-// Work decomposition:
-//   * one 1024-thread workgroup per CU (16 waves); the decode tables (hpk_code.h: 256 B T8 symbol
-//     table + 1.9 KiB leading-ones table) are staged into LDS once per workgroup;
-//   * every workgroup owns a contiguous range of literals (n / CUs) and stages it into one shared
-//     124 KiB LDS window: offsets with coalesced dword loads, literal bytes with 16-byte loads,
-//     every load issued before the first wait; ranges larger than the window take several fills;
-//   * per fill the workgroup builds a queue of 8-byte entries {window offset, length, output
-//     dword}; lanes decode one literal each out of LDS. Free lanes take the next queue slots every
-//     kRefillN steps (ballot + mbcnt) from a per-wave reservation that is topped up kChunk slots at
-//     a time with one LDS atomic on the block queue, so waves that the SIMD's age-priority
-//     arbitration favours simply take more literals, and long literals never hold up a wave;
-//   * a step refills the 64-bit bit window from a dword read one step ahead and decodes up to four
-//     codes speculatively as 5..8-bit codes: lengths from the canonical limits (no memory access
-//     on the serial chain), symbols from T8 off that chain. A 10..30-bit code parks the lane for
-//     one leading-ones lookup. Bits past the literal's end are NOT masked: a code that runs past
-//     the end is, by prefix-freeness, longer than what is left whatever follows, so the walk stops
-//     exactly where huffman.rs's bit iterator stops matching; only the final padding check
-//     (huffman.rs:128-160) looks at the residual bits, masked;
-//   * output bytes are packed in a register and stored as aligned dwords. A literal whose output
-//     region is not dword-aligned or is smaller than hpk_decoded_bound (caller-chosen offsets)
-//     is decoded after the queue drains with byte stores and per-byte capacity checks.
-// A literal too large for the LDS window is decoded by one lane straight from global memory.
+// Work decomposition (kernel template hpk_decode7 in hpk_decode_kernel.h, step 8):
+//   * one 1024-thread workgroup per CU (16 waves) owns a contiguous literal range (n / CUs); the
+//     decode tables (16 KiB two-symbol table, 1.9 KiB leading-ones table) are staged into LDS once;
+//   * the range is decoded in fills: a 40 KiB LDS input window, an LDS image of the fill's output
+//     span and a queue of up to 2048 literals ordered longest-first (counting sort on the encoded
+//     length: LPT list scheduling keeps the end-of-fill tail short). The next fill's offsets and
+//     window are loaded into registers while the current fill decodes, the previous fill's image
+//     is written back with 16-byte stores while it decodes; barriers order LDS only;
+//   * lanes decode one literal each out of LDS; free lanes take the next queue slots every 6 steps
+//     (ballot + mbcnt) from a per-wave reservation topped up 64 slots at a time with one LDS
+//     atomic, so waves the SIMD's age-priority arbitration favours simply take more literals;
+//   * a step refills a 64-bit bit window from a dword read one step ahead, looks the next 12 bits
+//     up in the two-symbol table and writes up to two symbols straight into the output image; a
+//     code longer than 12 bits (or EOS) takes one leading-ones lookup (any code in one read).
+//     Bits past a literal's end are NOT masked: a code that runs past the end is, by
+//     prefix-freeness, longer than what is left whatever follows, so the walk stops exactly where
+//     huffman.rs's bit iterator stops matching; only the final padding check (huffman.rs:128-160)
+//     looks at the residual bits, masked;
+//   * a literal whose output capacity is below hpk_decoded_bound (caller-chosen offsets) is decoded
+//     after the queue drains, code by code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
+// A literal too large for the window is decoded by one lane straight from global memory.
 #include <stdlib.h>
 
 #include "hpk_decode_kernel.h"
 
 using namespace hpkdec;
 
-// Product geometry (v7): 16 waves (one 1024-thread workgroup) per CU; per fill a 44 KiB input
-// window, an 84 KiB output image and a 2048-entry longest-first queue; lanes refill every 4
-// steps, waves reserve 64 queue slots at a time (chosen with bench/kvariants).
-constexpr int kWaves = 16, kW = 45056, kO = 86016, kQ = 2048, kRefillN = 4, kChunk = 64, kStep = 6;
-using Geo = Geo7<kWaves, kW, kO, kQ>;
+// Product geometry (v8): 16 waves (one 1024-thread workgroup) per CU; per fill a 40 KiB input
+// window, a 77 KiB output image and a 2048-entry longest-first queue, plus the 16 KiB two-symbol
+// table; lanes refill every 6 steps, waves reserve 64 queue slots at a time (bench/kvariants).
+constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 6, kChunk = 64, kStep = 8;
+using Geo = Geo7<kWaves, kW, kO, kQ, true>;
 #define DEC_KERNEL(m) hpk_decode7<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kStep>
 
 static int g_debug_mode = -1;
@@ -53,8 +52,7 @@ int hpk_decode_setup() {
                               reinterpret_cast<const void*>(&DEC_KERNEL(4))};
         rc = HPK_E_OK;
         for (int i = 0; i < 5 && rc == HPK_E_OK; ++i) {
-            hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, Geo::kLdsBytes);
-            if (e != hipSuccess) rc = hpk_set_err("hipFuncSetAttribute(decode LDS)", e);
+            (void)fns[i];  // the decode kernel's LDS is static (no dynamic-size attribute needed)
         }
         done = true;
     }
@@ -94,13 +92,14 @@ int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
     a.status = status;
     a.t8 = c->d_t8;
     a.lo = c->d_lo;
+    a.lut = c->d_lut;
     a.dbg = nullptr;
     // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
     uint64_t blocks = ((uint64_t)n + 63) / 64;
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
-    const int lds = Geo::kLdsBytes;
+    const int lds = 0;  // static LDS
     switch (g_debug_mode) {
         case 1:
             hipLaunchKernelGGL(DEC_KERNEL(1), grid, block, lds, c->stream, a);

@@ -25,6 +25,7 @@ struct DecodeArgs {
     uint8_t* status;
     const uint8_t* t8;
     const uint16_t* lo;
+    const uint32_t* lut;  // two-symbol table (hpk_code.h), step 8
     unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
 };
 
@@ -48,6 +49,18 @@ struct Lit {
 };
 
 enum StoreMode { kDword = 0, kNoStore = 1, kChecked = 3 };
+
+// Bitstream sources: a staged LDS window, or global memory (clamped to the batch).
+struct LdsSrc {
+    const uint32_t* p;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
+};
+struct GlobalSrc {
+    const uint32_t* p;
+    uint32_t last;  // last dword index holding a byte of the batch: never read past it
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[min(i, last)]; }
+};
+
 
 // diagnostic mode 4: record the first out-of-region store instead of performing it
 __device__ unsigned long long g_chk[8];
@@ -345,6 +358,285 @@ __device__ __forceinline__ void lit_unpark(Lit& L, const Src& src, const uint16_
     }
 }
 
+// v8 step: one lookup in the 12-bit two-symbol table (hpk_code.h LUT) decodes up to two codes
+// of <= 12 bits (the VALU work per symbol is a third of the arithmetic steps'; PMC showed those
+// saturating the SIMDs' vector issue). Symbols go straight to the LDS output image as bytes (no
+// accumulator), each under its own validity mask. A code longer than 12 bits (EOS included)
+// takes one leading-ones lookup in the (rarely taken) branch.
+template <int kStore, class Src>
+__device__ __forceinline__ void lit_step8(Lit& L, const Src& src, const uint32_t* __restrict__ lut,
+                                          const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8) {
+    lit_refill(L, src);
+    const uint32_t hi = (uint32_t)(L.win >> 32);
+    const uint32_t e = lut[hi >> (32 - HPK_LUT_BITS)];
+    const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+    const bool ok1 = L.live && (e >> 26) != 0u && len0 <= L.rem;
+    const bool ok2 = ok1 && (e >> 27) != 0u && tot <= L.rem;
+    const uint32_t use = ok2 ? tot : ok1 ? len0 : 0u;
+    const uint32_t pos = L.od + L.cnt;
+    if (kStore == kChecked) {
+        if (ok1 && L.cnt >= L.oend - L.od) chk_report(1, pos, L.oend, L.cnt);
+        if (ok2 && L.cnt + 1u >= L.oend - L.od) chk_report(1, pos + 1, L.oend, L.cnt);
+    }
+    if (kStore != kNoStore) {
+        if (ok1) out8[pos] = (uint8_t)e;
+        if (ok2) out8[pos + 1] = (uint8_t)(e >> 8);
+    } else {
+        asm volatile("" ::"v"(e));
+    }
+    L.cnt += (uint32_t)ok1 + (uint32_t)ok2;
+    L.win <<= use;
+    L.nb -= use;
+    L.rem -= use;
+    const bool park = L.live && (e >> 26) == 0u;  // a 13..30-bit code, or EOS
+    L.live = park || (ok1 && L.rem != 0u);
+    if (park) {
+        lit_refill(L, src);
+        const uint32_t w = (uint32_t)(L.win >> 32);
+        uint32_t s1, len;
+        bool eos;
+        lo_decode(w, lo, s1, len, eos);
+        if (len > L.rem) {
+            L.live = false;  // only padding left
+        } else if (eos) {
+            L.st = HPK_EOS_IN_STRING;  // huffman.rs:112-116
+            L.live = false;
+        } else {
+            if (kStore == kChecked && L.cnt >= L.oend - L.od) chk_report(1, L.od + L.cnt, L.oend, L.cnt);
+            if (kStore != kNoStore) out8[L.od + L.cnt] = (uint8_t)s1;
+            L.cnt += 1;
+            L.win <<= len;
+            L.nb -= len;
+            L.rem -= len;
+            L.live = L.rem != 0u;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// v9: bit-position decode, two literals per lane.
+//
+// PMC on the window-register steps (v6..v8): the SIMDs' vector issue was 70-90 % busy and half
+// the wave time sat in s_waitcnt on LDS. v9 keeps no bit window in registers: the input window
+// is staged byte-swapped (big-endian dwords), and each step reads the two dwords under the
+// literal's bit position P (one ds_read2), shifts them into a 32-bit window, and looks the next
+// 12 bits up in the two-symbol table: ~20 VALU per step instead of ~40. Each lane carries TWO
+// independent literals whose steps interleave, so one literal's LDS round trips hide behind the
+// other's arithmetic.
+struct Lit9 {
+    uint32_t P;    // bit position in the window (MSB-first over the big-endian dwords)
+    uint32_t E;    // end bit position
+    uint32_t cnt;  // bytes decoded
+    uint32_t od;   // output byte position in the LDS image
+    uint32_t oend; // checked mode: end of the output region
+    uint32_t w;    // the 32 bits at P from the last step (final padding check)
+    uint32_t e;    // the table entry of this step
+    uint32_t st;
+    bool live;
+};
+
+__device__ __forceinline__ uint32_t lit9_window(const uint32_t* __restrict__ win32, uint32_t P) {
+    const uint32_t q = P >> 5;
+    const uint64_t pair = ((uint64_t)win32[q] << 32) | win32[q + 1];
+    return (uint32_t)((pair << (P & 31u)) >> 32);
+}
+
+// Main part of a step (no branch): window, table entry, symbols, position.
+template <int kStore>
+__device__ __forceinline__ void lit9_main(Lit9& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                          uint8_t* __restrict__ out8) {
+    const uint32_t w = lit9_window(win32, L.P);
+    const uint32_t e = lut[w >> (32 - HPK_LUT_BITS)];
+    const uint32_t rem = L.E - L.P;
+    const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+    const bool ok1 = L.live && (e >> 26) != 0u && len0 <= rem;
+    const bool ok2 = ok1 && (e >> 27) != 0u && tot <= rem;
+    const uint32_t use = ok2 ? tot : ok1 ? len0 : 0u;
+    const uint32_t pos = L.od + L.cnt;
+    if (kStore == kChecked) {
+        if (ok1 && L.cnt >= L.oend - L.od) chk_report(1, pos, L.oend, L.cnt);
+        if (ok2 && L.cnt + 1u >= L.oend - L.od) chk_report(1, pos + 1, L.oend, L.cnt);
+    }
+    if (kStore != kNoStore) {
+        if (ok1) out8[pos] = (uint8_t)e;
+        if (ok2) out8[pos + 1] = (uint8_t)(e >> 8);
+    } else {
+        asm volatile("" ::"v"(e));
+    }
+    L.cnt += (uint32_t)ok1 + (uint32_t)ok2;
+    L.w = w;
+    L.e = e;
+    L.P += use;
+    // a code longer than 12 bits (or EOS) leaves the lane live with the entry's nsym = 0: the
+    // park part takes it; otherwise the literal goes on while bits are left
+    L.live = L.live && ((e >> 26) == 0u || (ok1 && L.P != L.E));
+}
+
+// Both literals of a lane in one step, all LDS reads issued before any LDS write: the byte
+// stores into the output image may alias the window / table as far as the compiler knows, so
+// reads placed after them could not be hoisted and the two literals' round trips would serialise.
+template <int kStore>
+__device__ __forceinline__ void lit9_pair(Lit9& A, Lit9& B, const uint32_t* __restrict__ win32,
+                                          const uint32_t* __restrict__ lut, uint8_t* __restrict__ out8) {
+    const uint32_t qa = A.P >> 5, qb = B.P >> 5;
+    const uint32_t a0 = win32[qa], a1 = win32[qa + 1], b0 = win32[qb], b1 = win32[qb + 1];
+    const uint32_t wa = (uint32_t)(((((uint64_t)a0 << 32) | a1) << (A.P & 31u)) >> 32);
+    const uint32_t wb = (uint32_t)(((((uint64_t)b0 << 32) | b1) << (B.P & 31u)) >> 32);
+    const uint32_t ea = lut[wa >> (32 - HPK_LUT_BITS)];
+    const uint32_t eb = lut[wb >> (32 - HPK_LUT_BITS)];
+    auto one = [&](Lit9& L, uint32_t w, uint32_t e, bool& ok1, bool& ok2, uint32_t& pos) {
+        const uint32_t rem = L.E - L.P;
+        const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+        // bitwise, not short-circuit: no branches between the two literals' work
+        ok1 = L.live & ((e >> 26) != 0u) & (len0 <= rem);
+        ok2 = ok1 & ((e >> 27) != 0u) & (tot <= rem);
+        const uint32_t use = ok2 ? tot : ok1 ? len0 : 0u;
+        pos = L.od + L.cnt;
+        if (kStore == kChecked) {
+            if (ok1 && L.cnt >= L.oend - L.od) chk_report(1, pos, L.oend, L.cnt);
+            if (ok2 && L.cnt + 1u >= L.oend - L.od) chk_report(1, pos + 1, L.oend, L.cnt);
+        }
+        L.cnt += (uint32_t)ok1 + (uint32_t)ok2;
+        L.w = w;
+        L.e = e;
+        L.P += use;
+        L.live = L.live & (((e >> 26) == 0u) | (ok1 & (L.P != L.E)));
+    };
+    bool a1ok, a2ok, b1ok, b2ok;
+    uint32_t pa, pb;
+    one(A, wa, ea, a1ok, a2ok, pa);
+    one(B, wb, eb, b1ok, b2ok, pb);
+    if (kStore != kNoStore) {
+        if (a1ok) out8[pa] = (uint8_t)ea;
+        if (a2ok) out8[pa + 1] = (uint8_t)(ea >> 8);
+        if (b1ok) out8[pb] = (uint8_t)eb;
+        if (b2ok) out8[pb + 1] = (uint8_t)(eb >> 8);
+    } else {
+        asm volatile("" ::"v"(ea), "v"(eb));
+    }
+}
+
+// Park part: the lanes whose entry had no code (a 13..30-bit code or EOS): leading-ones table.
+template <int kStore>
+__device__ __forceinline__ void lit9_park(Lit9& L, const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8) {
+    const uint32_t w = L.w;
+    uint32_t s1, len;
+    bool eos;
+    lo_decode(w, lo, s1, len, eos);
+    const uint32_t rem = L.E - L.P;
+    if (len > rem) {
+        L.live = false;  // only padding left
+    } else if (eos) {
+        L.st = HPK_EOS_IN_STRING;  // huffman.rs:112-116
+        L.live = false;
+    } else {
+        if (kStore == kChecked && L.cnt >= L.oend - L.od) chk_report(1, L.od + L.cnt, L.oend, L.cnt);
+        if (kStore != kNoStore) out8[L.od + L.cnt] = (uint8_t)s1;
+        L.cnt += 1;
+        L.P += len;
+        L.live = L.P != L.E;
+    }
+    L.e = 1u << 26;  // handled
+}
+
+__device__ __forceinline__ uint32_t lit9_status(const Lit9& L) {
+    uint32_t st = L.st;
+    const uint32_t rem = L.E - L.P;
+    if (st == HPK_OK && rem > 0) {  // huffman.rs:128-160
+        if (rem > 7)
+            st = HPK_PADDING_TOO_LARGE;
+        else if ((L.w | (0xFFFFFFFFu >> rem)) != 0xFFFFFFFFu)
+            st = HPK_INVALID_PADDING;
+    }
+    return st;
+}
+
+// The window as lit_begin/lit_refill expect it (raw byte order) for the byte path.
+struct LdsSwapSrc {
+    const uint32_t* p;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return __builtin_bswap32(p[i]); }
+};
+
+// v10 step: lit_step8 for two literals of a lane at once (kStep 10). All LDS reads of both
+// (prefetch dwords, table entries) are issued before any byte store, so the two literals' LDS
+// round trips overlap; the long-code branch runs once for both.
+template <int kStore>
+__device__ __forceinline__ void lit8_pair(Lit& A, Lit& B, const uint32_t* __restrict__ win32,
+                                          const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo,
+                                          uint8_t* __restrict__ out8) {
+    // refill both from their prefetched dwords; read the next prefetch dwords
+    auto refill_regs = [&](Lit& L) {
+        const bool need = L.nb <= 32u;
+        const uint64_t add = (uint64_t)__builtin_bswap32(L.nxt) << ((32u - L.nb) & 63u);
+        L.win |= need ? add : 0ull;
+        L.nb += need ? 32u : 0u;
+        L.nxt = need ? L.pf : L.nxt;
+        L.q += need ? 1u : 0u;
+    };
+    refill_regs(A);
+    refill_regs(B);
+    const uint32_t pfa = win32[A.q], pfb = win32[B.q];
+    const uint32_t ha = (uint32_t)(A.win >> 32), hb = (uint32_t)(B.win >> 32);
+    const uint32_t ea = lut[ha >> (32 - HPK_LUT_BITS)], eb = lut[hb >> (32 - HPK_LUT_BITS)];
+    A.pf = pfa;
+    B.pf = pfb;
+    auto one = [&](Lit& L, uint32_t e, bool& ok1, bool& ok2, uint32_t& pos) {
+        const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+        ok1 = L.live & ((e >> 26) != 0u) & (len0 <= L.rem);
+        ok2 = ok1 & ((e >> 27) != 0u) & (tot <= L.rem);
+        const uint32_t use = ok2 ? tot : ok1 ? len0 : 0u;
+        pos = L.od + L.cnt;
+        if (kStore == kChecked) {
+            if (ok1 && L.cnt >= L.oend - L.od) chk_report(1, pos, L.oend, L.cnt);
+            if (ok2 && L.cnt + 1u >= L.oend - L.od) chk_report(1, pos + 1, L.oend, L.cnt);
+        }
+        L.cnt += (uint32_t)ok1 + (uint32_t)ok2;
+        L.win <<= use;
+        L.nb -= use;
+        L.rem -= use;
+        L.park = L.live & ((e >> 26) == 0u);  // a 13..30-bit code, or EOS
+        L.live = L.park | (ok1 & (L.rem != 0u));
+    };
+    bool a1, a2, b1, b2;
+    uint32_t pa, pb;
+    one(A, ea, a1, a2, pa);
+    one(B, eb, b1, b2, pb);
+    if (kStore != kNoStore) {
+        if (a1) out8[pa] = (uint8_t)ea;
+        if (a2) out8[pa + 1] = (uint8_t)(ea >> 8);
+        if (b1) out8[pb] = (uint8_t)eb;
+        if (b2) out8[pb + 1] = (uint8_t)(eb >> 8);
+    } else {
+        asm volatile("" ::"v"(ea), "v"(eb));
+    }
+    if (__any(A.park | B.park)) {
+        auto park = [&](Lit& L) {
+            L.park = false;
+            lit_refill(L, LdsSrc{win32});
+            const uint32_t w = (uint32_t)(L.win >> 32);
+            uint32_t s1, len;
+            bool eos;
+            lo_decode(w, lo, s1, len, eos);
+            if (len > L.rem) {
+                L.live = false;  // only padding left
+            } else if (eos) {
+                L.st = HPK_EOS_IN_STRING;  // huffman.rs:112-116
+                L.live = false;
+            } else {
+                if (kStore == kChecked && L.cnt >= L.oend - L.od) chk_report(1, L.od + L.cnt, L.oend, L.cnt);
+                if (kStore != kNoStore) out8[L.od + L.cnt] = (uint8_t)s1;
+                L.cnt += 1;
+                L.win <<= len;
+                L.nb -= len;
+                L.rem -= len;
+                L.live = L.rem != 0u;
+            }
+        };
+        if (A.park) park(A);
+        if (B.park) park(B);
+    }
+}
+
 // Final status of a literal whose walk has stopped (huffman.rs:128-160): at most 7 residual
 // bits, all ones (the most significant bits of EOS); an EOS decoded inside wins (st already set).
 __device__ __forceinline__ uint32_t lit_status(const Lit& L) {
@@ -414,15 +706,6 @@ __device__ __forceinline__ void lit_bytes(const Src& src, const uint16_t* lo, co
     lit_finish<kNoStore>(L, a, i);
 }
 
-struct LdsSrc {
-    const uint32_t* p;
-    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
-};
-struct GlobalSrc {
-    const uint32_t* p;
-    uint32_t last;  // last dword index holding a byte of the batch: never read past it
-    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[min(i, last)]; }
-};
 
 // Block-level window (v5): the workgroup stages a contiguous run of its literals into one LDS
 // window shared by all its waves, and every wave pulls literals from ONE block queue (an LDS
@@ -634,13 +917,15 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode_kernel(DecodeArgs a) {
 // output image (1.6x + rounding) and the queue, so fills are ~2.5x smaller; the load balance
 // that costs is won back by ordering each fill's queue longest-first (a counting sort on the
 // encoded length: LPT list scheduling, the tail is made of short literals).
-template <int kWaves, int kW, int kO, int kQ>
+template <int kWaves, int kW, int kO, int kQ, bool kLut = false>
 struct Geo7 {
     static constexpr int kBlock = kWaves * 64;
     static constexpr int kMetaRounds = (kQ + kBlock - 1) / kBlock;
     static constexpr int kStageRounds = (kW / 16 + kBlock - 1) / kBlock;
     static constexpr int kFlushRounds = (kO / 16 + 1 + kBlock - 1) / kBlock;
-    static constexpr int kInOff = kTabBytes;
+    static constexpr int kLutBytes = kLut ? (int)(HPK_LUT_SIZE * 4) : 0;
+    static constexpr int kLutOff = kTabBytes;
+    static constexpr int kInOff = kTabBytes + kLutBytes;
     static constexpr int kOutOff = kInOff + kW;
     static constexpr int kQOff = kOutOff + kO;
     static constexpr int kLenOff = kQOff + 8 * kQ;
@@ -649,7 +934,7 @@ struct Geo7 {
     static constexpr int kLdsBytes = kCtrOff + 16;
     static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
     static_assert(kW % 16 == 0 && kW <= 65536, "window offsets and lengths pack in 16 bits");
-    static_assert(kO % 16 == 0 && kO / 4 <= 32768, "output dword index packs in 15 bits");
+    static_assert(kO % 16 == 0 && kO <= 131072, "output byte offset packs in 17 bits");
     static_assert(kQ <= 4096, "fill index packs in 12 bits");
 };
 constexpr uint32_t kQ7Byte = 0x80000000u;  // queue entry .y flag: byte path
@@ -725,11 +1010,12 @@ __device__ __forceinline__ void prefetch_fill(Prefetch<kMeta, kStage>& P, const 
 // (queue build, window copy, flush reads) sits between two decodes.
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kStep>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
-    using G = Geo7<kWaves, kW, kO, kQ>;
+    using G = Geo7<kWaves, kW, kO, kQ, (kStep >= 8)>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
     unsigned long long t_start = 0, t_staged = 0;
     if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // static LDS: the compiler folds every region offset into the ds instructions' offset fields
+    __shared__ __attribute__((aligned(16))) uint8_t smem[G::kLdsBytes];
     uint8_t* s_t8 = smem;
     uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
     uint8_t* s_in = smem + G::kInOff;
@@ -745,6 +1031,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
         reinterpret_cast<uint4*>(s_t8)[t] = reinterpret_cast<const uint4*>(a.t8)[t];
     for (uint32_t t = threadIdx.x; t < kLoBytes / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+    uint32_t* s_lut = reinterpret_cast<uint32_t*>(smem + G::kLutOff);
+    if (kStep >= 8)
+        for (uint32_t t = threadIdx.x; t < (uint32_t)G::kLutBytes / 16; t += G::kBlock)
+            reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut)[t];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -753,6 +1043,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
     const uint32_t in_end = a.in_off[a.n] + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
+    // last chunk holding a byte of THIS workgroup's literals: windows never read past it (the
+    // next workgroup reads its own range), and the final, unused prefetch collapses onto it
+    const uint32_t r_end = a.in_off[BB] + a.in_mis;
+    const uint32_t rlast16 = r_end ? (r_end - 1) >> 4 : 0;
 
     // write back one decoded fill from the LDS image: the output span [G0, G1) with 16-byte
     // stores (bytewise in the two end chunks, which neighbours own), then out_len and status
@@ -794,7 +1088,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
     if (cur < BB) {
         gin = a.in_off[cur] + a.in_mis;
         gout = a.out_off[cur] + a.out_mis;
-        prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, last16);
+        prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
     }
     while (cur < BB) {  // block-uniform
         const uint32_t cntl = min((uint32_t)kQ, BB - cur);
@@ -804,7 +1098,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
         if (tid < 64) s_hist[tid] = 0;
         if (tid == 0) {
             s_ctr[0] = 0;
-            s_ctr[1] = G::kBlock;
+            s_ctr[1] = kStep >= 9 ? 2 * G::kBlock : G::kBlock;  // slots handed out at the start
             s_ctr[2] = gin;
             s_ctr[3] = gout;
         }
@@ -821,10 +1115,11 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
             pos[r] = 0xFFFFFFFFu;
             if (fits) {
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
-                // dword path: aligned region holding hpk_decoded_bound(nbytes) bytes
-                const bool dw = ((o0 | ocap) & 3u) == 0 && ocap >= (nbytes * 8u) / 5u;
+                // fast path: a region holding hpk_decoded_bound(nbytes) bytes (dword-aligned for
+                // the accumulator steps, which store whole dwords)
+                const bool dw = (kStep >= 8 || ((o0 | ocap) & 3u) == 0) && ocap >= (nbytes * 8u) / 5u;
                 ex[r] = (p0 - base16) | (nbytes << 16);
-                ey[r] = t | (((o0 - ob16) >> 2) << 12) | (dw ? 0u : kQ7Byte);
+                ey[r] = t | ((o0 - ob16) << 12) | (dw ? 0u : kQ7Byte);
                 const uint32_t bk = lpt_bucket(nbytes);
                 pos[r] = (bk << 16) | atomicAdd(&s_hist[bk], 1u);
             }
@@ -857,7 +1152,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
             if (cur < BB) {
                 gin = a.in_off[cur] + a.in_mis;
                 gout = a.out_off[cur] + a.out_mis;
-                prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, last16);
+                prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
             }
             continue;
         }
@@ -877,8 +1172,13 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
         {
             uint4* l16 = reinterpret_cast<uint4*>(s_in);
 #pragma unroll
-            for (int r = 0; r < S; ++r)
-                if (tid + G::kBlock * r < kW / 16) l16[tid + G::kBlock * r] = P.chunk[r];
+            for (int r = 0; r < S; ++r) {
+                uint4 c = P.chunk[r];
+                if (kStep == 9)  // big-endian dwords: bit P of the stream is bit 31 - P % 32 of dword P / 32
+                    c = make_uint4(__builtin_bswap32(c.x), __builtin_bswap32(c.y), __builtin_bswap32(c.z),
+                                   __builtin_bswap32(c.w));
+                if (tid + G::kBlock * r < kW / 16) l16[tid + G::kBlock * r] = c;
+            }
         }
         lds_barrier();
 #pragma unroll
@@ -889,8 +1189,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
         const uint32_t cur_next = cur + k;
         {
             const uint32_t c = min(cur_next, BB - 1);
-            prefetch_fill<G::kBlock>(P, a, tid, c, min(c + (uint32_t)kQ, BB), min(gin_next, in_end ? in_end - 1 : 0) & ~15u,
-                                     last16);
+            prefetch_fill<G::kBlock>(P, a, tid, c, min(c + (uint32_t)kQ, BB), gin_next & ~15u, rlast16);
         }
         // the previous fill's write-back: its image is read out before this fill decodes over it
         if (pk) flush(pcur, pk, pG0, pG1);
@@ -905,6 +1204,169 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
                 const uint2 e = s_q[t];
                 s_lenst[e.y & 0xFFFu] = (e.x >> 16) + s_in[e.x & 0xFFFFu];
             }
+        } else if (kStep == 10) {
+            constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
+            static_assert(kStep != 10 || kChunk >= 128, "a refill can hand out 128 slots (two per lane)");
+            const uint32_t* win32 = reinterpret_cast<const uint32_t*>(s_in);
+            Lit A = {}, B = {};  // every field defined: idle lanes still run the (predicated) step
+            A.nb = 64;
+            B.nb = 64;
+            uint32_t ta = tid, tb = tid + G::kBlock;
+            uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
+            bool acta = false, actb = false;
+            uint32_t ia = 0, ib = 0;
+            auto begin = [&](Lit& L, bool& act, uint32_t& idx, uint32_t tt) {
+                const uint2 e = s_q[min(tt, k - 1)];
+                act = tt < k && !(e.y & kQ7Byte);
+                idx = e.y & 0xFFFu;
+                lit_begin(L, lds, e.x & 0xFFFFu, e.x >> 16);
+                L.park = false;
+                L.od = (e.y >> 12) & 0x1FFFFu;
+                L.oend = L.od + (e.x >> 16) * 8u / 5u;
+                L.live = L.live && act;
+            };
+            begin(A, acta, ia, ta);
+            begin(B, actb, ib, tb);
+            for (;;) {
+#pragma unroll
+                for (int s = 0; s < kRefillN; ++s) lit8_pair<kStore>(A, B, win32, s_lut, s_lo, s_out);
+                const bool fa = ta < k && !A.live, fb = tb < k && !B.live;
+                if (__any(fa || fb)) {
+                    if (fa && acta) s_lenst[ia] = A.cnt | (lit_status(A) << 24);
+                    if (fb && actb) s_lenst[ib] = B.cnt | (lit_status(B) << 24);
+                    const bool fra = fa || ta >= k, frb = fb || tb >= k;
+                    const uint64_t ma = __ballot(fra), mb = __ballot(frb);
+                    const uint32_t na = (uint32_t)__popcll(ma);
+                    const uint32_t ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+                    const uint32_t rb =
+                        na + __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+                    const uint32_t need = na + (uint32_t)__popcll(mb), have = qe - qb;
+                    uint32_t nb = qb;
+                    if (have < need) {  // wave-uniform: reserve kChunk more slots
+                        uint32_t g = 0;
+                        if (lane == 0) g = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
+                        g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+                        nb = g;
+                    }
+                    const uint32_t xa = ra < have ? qb + ra : nb + (ra - have);
+                    const uint32_t xb = rb < have ? qb + rb : nb + (rb - have);
+                    if (have < need) {
+                        qb = nb + (need - have);
+                        qe = nb + kChunk;
+                    } else {
+                        qb += need;
+                    }
+                    qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
+                    qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
+                    if (fra) {
+                        ta = xa;
+                        begin(A, acta, ia, xa);
+                    }
+                    if (frb) {
+                        tb = xb;
+                        begin(B, actb, ib, xb);
+                    }
+                }
+                if (!__any(ta < k || tb < k)) break;
+            }
+            for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
+                const uint2 e = s_q[tt];
+                if (e.y & kQ7Byte) {
+                    const uint32_t i = e.y & 0xFFFu;
+                    const uint32_t o = a.out_off[cur + i] + a.out_mis - ob16;
+                    Lit Bt = {};
+                    lit_bytes_to(Bt, lds, s_lo, [&](uint32_t j, uint8_t v) { s_out[o + j] = v; },
+                                 a.out_off[cur + i + 1] - a.out_off[cur + i], e.x & 0xFFFFu, e.x >> 16);
+                    s_lenst[i] = Bt.cnt | (lit_status(Bt) << 24);
+                }
+            }
+        } else if (kStep == 9) {
+            constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
+            static_assert(kStep != 9 || kChunk >= 128, "a refill can hand out 128 slots (two per lane)");
+            const uint32_t* win32 = reinterpret_cast<const uint32_t*>(s_in);
+            Lit9 A = {}, B = {};
+            uint32_t ta = tid, tb = tid + G::kBlock;
+            uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
+            bool acta = false, actb = false;
+            uint32_t ia = 0, ib = 0;
+            auto begin = [&](Lit9& L, bool& act, uint32_t& idx, uint32_t tt) {
+                const uint2 e = s_q[min(tt, k - 1)];
+                act = tt < k && !(e.y & kQ7Byte);
+                idx = e.y & 0xFFFu;
+                L.P = (e.x & 0xFFFFu) * 8u;
+                L.E = L.P + (e.x >> 16) * 8u;
+                L.cnt = 0;
+                L.st = HPK_OK;
+                L.w = 0xFFFFFFFFu;
+                L.e = 1u << 26;
+                L.od = (e.y >> 12) & 0x1FFFFu;
+                L.oend = L.od + (e.x >> 16) * 8u / 5u;
+                L.live = act && L.P != L.E;
+            };
+            begin(A, acta, ia, ta);
+            begin(B, actb, ib, tb);
+            for (;;) {
+#pragma unroll
+                for (int s = 0; s < kRefillN; ++s) {
+                    lit9_pair<kStore>(A, B, win32, s_lut, s_out);
+                    const bool pa = A.live && (A.e >> 26) == 0u, pb = B.live && (B.e >> 26) == 0u;
+                    if (__any(pa || pb)) {
+                        if (pa) lit9_park<kStore>(A, s_lo, s_out);
+                        if (pb) lit9_park<kStore>(B, s_lo, s_out);
+                    }
+                }
+                const bool fa = ta < k && !A.live, fb = tb < k && !B.live;
+                if (__any(fa || fb)) {
+                    if (fa && acta) s_lenst[ia] = A.cnt | (lit9_status(A) << 24);
+                    if (fb && actb) s_lenst[ib] = B.cnt | (lit9_status(B) << 24);
+                    const bool fra = fa || ta >= k, frb = fb || tb >= k;
+                    const uint64_t ma = __ballot(fra), mb = __ballot(frb);
+                    const uint32_t na = (uint32_t)__popcll(ma);
+                    const uint32_t ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+                    const uint32_t rb =
+                        na + __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+                    const uint32_t need = na + (uint32_t)__popcll(mb), have = qe - qb;
+                    uint32_t nb = qb;
+                    if (have < need) {  // wave-uniform: reserve kChunk more slots
+                        uint32_t g = 0;
+                        if (lane == 0) g = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
+                        g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+                        nb = g;
+                    }
+                    // rank r takes qb + r while r < have, else nb + (r - have)
+                    const uint32_t xa = ra < have ? qb + ra : nb + (ra - have);
+                    const uint32_t xb = rb < have ? qb + rb : nb + (rb - have);
+                    if (have < need) {
+                        qb = nb + (need - have);
+                        qe = nb + kChunk;
+                    } else {
+                        qb += need;
+                    }
+                    qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
+                    qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
+                    if (fra) {
+                        ta = xa;
+                        begin(A, acta, ia, xa);
+                    }
+                    if (frb) {
+                        tb = xb;
+                        begin(B, actb, ib, xb);
+                    }
+                }
+                if (!__any(ta < k || tb < k)) break;
+            }
+            // byte path (capacity below the decoded bound)
+            for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
+                const uint2 e = s_q[tt];
+                if (e.y & kQ7Byte) {
+                    const uint32_t i = e.y & 0xFFFu;
+                    const uint32_t o = a.out_off[cur + i] + a.out_mis - ob16;
+                    Lit Bt = {};
+                    lit_bytes_to(Bt, LdsSwapSrc{win32}, s_lo, [&](uint32_t j, uint8_t v) { s_out[o + j] = v; },
+                                 a.out_off[cur + i + 1] - a.out_off[cur + i], e.x & 0xFFFFu, e.x >> 16);
+                    s_lenst[i] = Bt.cnt | (lit_status(Bt) << 24);
+                }
+            }
         } else {
             constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
             Lit L = {};  // every field defined: idle lanes still run the (predicated) step
@@ -918,15 +1380,18 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
                 act = tt < k && !(e.y & kQ7Byte);
                 idx = e.y & 0xFFFu;
                 lit_begin(L, lds, e.x & 0xFFFFu, e.x >> 16);
-                L.od = (e.y >> 12) & 0x7FFFu;
-                L.oend = L.od + ((e.x >> 16) * 8u / 5u + 3u) / 4u;
+                const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
+                L.od = kStep == 8 ? ob : ob >> 2;  // byte (step 8) or dword position in the image
+                L.oend = kStep == 8 ? ob + (e.x >> 16) * 8u / 5u : L.od + ((e.x >> 16) * 8u / 5u + 3u) / 4u;
                 L.live = L.live && act;
             };
             begin(t);
             for (;;) {
 #pragma unroll
                 for (int s = 0; s < kRefillN; ++s) {
-                    if (kStep == 7)
+                    if (kStep == 8)
+                        lit_step8<kStore>(L, lds, s_lut, s_lo, s_out);
+                    else if (kStep == 7)
                         lit_step7<kStore>(L, lds, s_t8, s_out);
                     else if (kStep == 6)
                         lit_step6<kStore>(L, lds, s_t8, s_lo, s_out);
@@ -939,8 +1404,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode7(DecodeArgs a) {
                 const bool fin = t < k && !L.live;
                 if (__any(fin)) {
                     if (fin && act) {
-                        if (kStore == kDword && L.accn) s_out32[L.od] = (uint32_t)L.acc;
-                        if (kStore == kChecked && L.accn) {
+                        if (kStep != 8 && kStore == kDword && L.accn) s_out32[L.od] = (uint32_t)L.acc;
+                        if (kStep != 8 && kStore == kChecked && L.accn) {
                             if (L.od < L.oend && L.od < (uint32_t)kO / 4)
                                 s_out32[L.od] = (uint32_t)L.acc;
                             else

@@ -14,6 +14,7 @@ struct hpk_ctx {
     int num_cu = 256;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
+    uint32_t* d_lut = nullptr;
     uint16_t* d_lo = nullptr;
     uint8_t* d_t8 = nullptr;
     uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length

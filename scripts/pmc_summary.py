@@ -12,15 +12,14 @@ data = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        m = re.search(r"hpk_decode_kernel<(.*?)>|hpk_decode_kernelILi(\d+)ELi(\d+)ELi(\d+)E|hpk_decode_kernelILi(\d+)E", k)
         if "decode" not in k:
             continue
-        if m and m.group(1):
-            name = m.group(1)
-        elif m and m.group(2):
-            name = f"{m.group(2)},{m.group(3)},{m.group(4)}"
+        m = re.search(r"(hpk_decode\w*?)I((?:Li\d+E)+)", k)
+        if m:
+            name = m.group(1) + "<" + ",".join(re.findall(r"Li(\d+)E", m.group(2))) + ">"
         else:
-            name = k[:40]
+            m = re.search(r"(hpk_decode\w*<[^>]*>)", k)
+            name = m.group(1) if m else k[:60]
         data[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for name, ctrs in data.items():
     waves = sum(ctrs["SQ_WAVES"]) / max(1, len(ctrs["SQ_WAVES"])) if "SQ_WAVES" in ctrs else 4096
