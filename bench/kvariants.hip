@@ -8,7 +8,7 @@
 
 #include <vector>
 
-#include "../loona_amd/csrc/hpk_decode_kernel.h"
+#include "../loona_amd/csrc/hpk_decode11.h"
 
 using namespace hpkdec;
 
@@ -88,6 +88,15 @@ static void run7(const char* name, Dev& d, const std::vector<uint32_t>& ref_len,
                   d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
+// v11: one big window per fill, output dwords straight to global
+template <int kMode, int kWaves, int kW, int kQ, int kR, int kC, bool kLpt = true>
+static void run11(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
+                  const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
+    using G = Geo11<kWaves, kW, kQ>;
+    run_fn<kMode>(name, hpk_decode11<kMode, kWaves, kW, kQ, kR, kC, kLpt>, 0, G::kBlock, 1, d, ref_len, ref_st, ref_out,
+                  num_cu, iters);
+}
+
 extern "C" int hpk_decode_batch_cpu(const uint8_t*, const uint32_t*, uint32_t, uint8_t*, const uint32_t*, uint32_t*,
                                     uint8_t*, int);
 
@@ -152,11 +161,9 @@ int main(int argc, char** argv) {
     const int cu = prop.multiProcessorCount;
     printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
     run7<0, 16, 40960, 79104, 2048, 6, 64, 8>("v8_r6", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<4, 16, 40960, 79104, 2048, 4, 128, 10>("v10_r4_checked", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 40960, 79104, 2048, 3, 128, 10>("v10_r3", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 40960, 79104, 2048, 4, 128, 10>("v10_r4", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<0, 16, 40960, 79104, 2048, 6, 128, 10>("v10_r6", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<2, 16, 40960, 79104, 2048, 4, 128, 10>("v10_r4_nostore", d, ref_len, ref_st, ref_out, cu, iters);
-    run7<1, 16, 40960, 79104, 2048, 4, 128, 10>("v10_stage", d, ref_len, ref_st, ref_out, cu, iters);
+    run11<0, 16, 111984, 4096, 6, 64, false>("v11_r6_order", d, ref_len, ref_st, ref_out, cu, iters);
+    run11<0, 16, 111984, 4096, 8, 64, false>("v11_r8_order", d, ref_len, ref_st, ref_out, cu, iters);
+    run11<2, 16, 111984, 4096, 6, 64, false>("v11_r6_order_nostore", d, ref_len, ref_st, ref_out, cu, iters);
+    run11<0, 16, 111984, 4096, 8, 64>("v11_r8", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }
