@@ -11,7 +11,7 @@ Multi-GPU (`--gpus N` under torch.distributed.run): weak scaling, each rank deco
 bytes / max time.
 
 Extras on the JSON line:
-  roofline      dominant kernel (hpk_decode7): algorithmic bytes per launch
+  roofline      dominant kernel (hpk_decode12): algorithmic bytes per launch
                 (sum of enc + dec + 13 per literal) / average launch time, against
                 the 8.0 TB/s HBM3E spec peak; traffic = PMC HBM bytes per launch from the
                 committed rocprofv3 counter summary (profiles/), null when absent
@@ -240,7 +240,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "hpk_decode7",
+                "kernel": "hpk_decode12",
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
             },

@@ -6,9 +6,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../loona_amd/csrc/hpk_decode11.h"
+#include "../loona_amd/csrc/hpk_decode12.h"
 
 using namespace hpkdec;
 
@@ -97,11 +99,52 @@ static void run11(const char* name, Dev& d, const std::vector<uint32_t>& ref_len
                   num_cu, iters);
 }
 
+// v12: bit-position step (kLook lookups per step, byte or dword stores) + cooperative long literals
+static const char* g_only = nullptr;  // run only the variant of this name (argv[3])
+
+template <int kMode, int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048,
+          int kCoop = 1>
+static void run12(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
+                  const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
+    if (g_only && strcmp(g_only, name) != 0) return;
+    using G = Geo12<kWaves, kW, kO, kQ>;
+    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop>, 0, G::kBlock, 1, d,
+                  ref_len, ref_st, ref_out, num_cu, iters);
+}
+
+// v12 diagnostic stamps (kMode 3): per wave total cycles, cycles in the decode phases, steps, fills
+template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048>
+static void stamps12(const char* name, Dev& d, int num_cu) {
+    using G = Geo12<kWaves, kW, kO, kQ>;
+    const size_t nw = (size_t)num_cu * kWaves;
+    unsigned long long* dbg;
+    CK(hipMalloc(&dbg, nw * 4 * 8));
+    DecodeArgs a = d.a;
+    a.dbg = dbg;
+    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc>;
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(num_cu), dim3(G::kBlock), 0, 0, a);
+    CK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(nw * 4);
+    CK(hipMemcpy(h.data(), dbg, nw * 32, hipMemcpyDeviceToHost));
+    double s[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+    for (size_t w = 0; w < nw; ++w)
+        for (int j = 0; j < 4; ++j) {
+            s[j] += (double)h[w * 4 + j];
+            mx[j] = std::max(mx[j], (double)h[w * 4 + j]);
+        }
+    printf("{\"stamps\": \"%s\", \"cycles_mean\": %.0f, \"cycles_max\": %.0f, \"decode_cycles_mean\": %.0f, "
+           "\"decode_cycles_max\": %.0f, \"steps_mean\": %.1f, \"steps_max\": %.0f, \"fills_mean\": %.2f}\n",
+           name, s[0] / nw, mx[0], s[1] / nw, mx[1], s[2] / nw, mx[2], s[3] / nw);
+    fflush(stdout);
+    CK(hipFree(dbg));
+}
+
 extern "C" int hpk_decode_batch_cpu(const uint8_t*, const uint32_t*, uint32_t, uint8_t*, const uint32_t*, uint32_t*,
                                     uint8_t*, int);
 
 int main(int argc, char** argv) {
     if (argc < 2) return 1;
+    setvbuf(stdout, nullptr, _IOLBF, 0);
     FILE* f = fopen(argv[1], "rb");
     uint32_t n, eb;
     if (fread(&n, 4, 1, f) != 1 || fread(&eb, 4, 1, f) != 1) return 1;
@@ -137,6 +180,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_lo, sizeof(tab.lo)));
     CK(hipMalloc(&d_lut2, sizeof(tab.lut)));
     CK(hipMemcpy(d_lut2, tab.lut, sizeof(tab.lut), hipMemcpyHostToDevice));
+    uint32_t* d_lut3;
+    CK(hipMalloc(&d_lut3, sizeof(tab.lut2)));
+    CK(hipMemcpy(d_lut3, tab.lut2, sizeof(tab.lut2), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_in, blob.data(), eb, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_io, in_off.data(), (n + 1) * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_oo, out_off.data(), (n + 1) * 4, hipMemcpyHostToDevice));
@@ -155,15 +201,23 @@ int main(int argc, char** argv) {
     a.t8 = reinterpret_cast<const uint8_t*>(d_lut);
     a.lo = d_lo;
     a.lut = d_lut2;
+    a.lut2 = d_lut3;
     a.dbg = nullptr;
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int cu = prop.multiProcessorCount;
     printf("{\"n\": %u, \"enc_bytes\": %u, \"cus\": %d}\n", n, eb, cu);
+    if (argc > 3) {  // one named variant per process (a hang then names itself)
+        g_only = argv[3];
+        run12<0, 3, 2, false, 16, 40960, 79104, 2048, 0>("coop0", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 3, 2, false, 16, 40960, 79104, 2048, 2>("coop2", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 3, 2, false, 16, 40960, 79104, 2048, 3>("coop3", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<4, 3, 2, false>("coop1_checked", d, ref_len, ref_st, ref_out, cu, 1);
+        run12<0, 3, 2, false>("coop1", d, ref_len, ref_st, ref_out, cu, iters);
+        return 0;
+    }
     run7<0, 16, 40960, 79104, 2048, 6, 64, 8>("v8_r6", d, ref_len, ref_st, ref_out, cu, iters);
-    run11<0, 16, 111984, 4096, 6, 64, false>("v11_r6_order", d, ref_len, ref_st, ref_out, cu, iters);
-    run11<0, 16, 111984, 4096, 8, 64, false>("v11_r8_order", d, ref_len, ref_st, ref_out, cu, iters);
-    run11<2, 16, 111984, 4096, 6, 64, false>("v11_r6_order_nostore", d, ref_len, ref_st, ref_out, cu, iters);
-    run11<0, 16, 111984, 4096, 8, 64>("v11_r8", d, ref_len, ref_st, ref_out, cu, iters);
+    run12<0, 3, 2, false>("v12_l2b_r3", d, ref_len, ref_st, ref_out, cu, iters);
+    run12<0, 3, 2, true>("v12_l2a_r3", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }

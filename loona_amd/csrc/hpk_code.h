@@ -56,10 +56,18 @@ static const uint8_t HPK_CODE_LEN[HPK_NSYM] = {
     30,                                                             /* EOS      */
 };
 
+// LUT2: the LUT's content in the layout of the bit-position step (decode v12), chosen so the step
+// needs one compare per field and v_perm gathers the two symbols:
+//   [7:0] sym0  [12:8] len0  [23:16] sym1  [28:24] len0+len1  [30] one code  [31:30] = 3: two
+// so e >= HPK_LUT2_ONE  <=> at least one code, e >= HPK_LUT2_TWO <=> two codes.
+#define HPK_LUT2_ONE 0x40000000u
+#define HPK_LUT2_TWO 0xC0000000u
+
 struct hpk_tables {
     uint32_t code[HPK_NSYM];   // right-aligned canonical code
     uint8_t len[HPK_NSYM];     // code length in bits
     uint32_t lut[HPK_LUT_SIZE];
+    uint32_t lut2[HPK_LUT_SIZE];
     uint16_t lo[HPK_LO_SIZE];
     uint8_t t8[256];  // symbol of the <=8-bit code that prefixes each 8-bit window (0 past LIM8)
 };
@@ -122,7 +130,7 @@ static inline int hpk_build_tables(hpk_tables* t) {
             int L = t->len[s];
             if (L <= HPK_LUT_BITS && (w >> (32 - L)) == t->code[s]) { s0 = s; l0 = L; break; }
         }
-        if (s0 < 0) { t->lut[v] = 0; continue; }
+        if (s0 < 0) { t->lut[v] = 0; t->lut2[v] = 0; continue; }
         uint32_t w1 = w << l0;
         int rem = HPK_LUT_BITS - l0, s1 = -1, l1 = 0;
         for (int s = 0; s < 256 && rem >= 5; ++s) {
@@ -130,11 +138,16 @@ static inline int hpk_build_tables(hpk_tables* t) {
             if (L <= rem && (w1 >> (32 - L)) == t->code[s]) { s1 = s; l1 = L; break; }
         }
         uint32_t e = (uint32_t)s0 | ((uint32_t)l0 << 16);
-        if (s1 >= 0)
+        uint32_t e2 = (uint32_t)s0 | ((uint32_t)l0 << 8);
+        if (s1 >= 0) {
             e |= ((uint32_t)s1 << 8) | ((uint32_t)(l0 + l1) << 21) | (2u << 26);
-        else
+            e2 |= ((uint32_t)s1 << 16) | ((uint32_t)(l0 + l1) << 24) | HPK_LUT2_TWO;
+        } else {
             e |= ((uint32_t)l0 << 21) | (1u << 26);
+            e2 |= ((uint32_t)l0 << 24) | HPK_LUT2_ONE;
+        }
         t->lut[v] = e;
+        t->lut2[v] = e2;
     }
     return 0;
 }

@@ -4,7 +4,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.8 gfx950 decode v8 (two-symbol LDS table, LDS output image, longest-first queue, pipelined fills)"
+#define HPK_VERSION "hpk 0.12 gfx950 decode v12 (alignbit bit-position step, two lookups per step, cooperative long literals, LDS image, longest-first queue)"
 
 static thread_local std::string t_last_error;
 
@@ -52,6 +52,9 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     c->stream = c->own;
     if ((e = hipMalloc(&c->d_lut, sizeof(t->lut))) != hipSuccess) return fail("hipMalloc lut", e);
     if ((e = hipMemcpy(c->d_lut, t->lut, sizeof(t->lut), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload lut", e);
+    if ((e = hipMalloc(&c->d_lut2, sizeof(t->lut2))) != hipSuccess) return fail("hipMalloc lut2", e);
+    if ((e = hipMemcpy(c->d_lut2, t->lut2, sizeof(t->lut2), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail("upload lut2", e);
     if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
     if ((e = hipMalloc(&c->d_t8, sizeof(t->t8))) != hipSuccess) return fail("hipMalloc t8", e);
     if ((e = hipMemcpy(c->d_t8, t->t8, sizeof(t->t8), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload t8", e);
@@ -71,6 +74,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->d_lut);
+    (void)hipFree(c->d_lut2);
     (void)hipFree(c->d_lo);
     (void)hipFree(c->d_t8);
     (void)hipFree(c->d_codes);

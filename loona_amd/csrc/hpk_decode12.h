@@ -1,0 +1,682 @@
+// hpk_decode12.h — decode kernel v12: the v8 fill structure, a bit-position step, and a
+// wave-cooperative path for long literals.
+//
+// Fill structure as v8 (hpk_decode7 in hpk_decode_kernel.h): per fill an LDS input window, an LDS
+// image of the fill's output span and a longest-first queue; the next fill's offsets and window
+// are prefetched into registers while the current one decodes, the previous image is written
+// back with 16-byte stores. What changes:
+//   * the window is staged as big-endian dwords; a lane holds its bit position as X = P + 31 and
+//     the dword pair (d0, d1) = window dwords (X >> 5) - 1 and X >> 5, plus the next dword d2.
+//     The 32 bits at P are ONE v_alignbit_b32(d0, d1, ~X): no 64-bit shifts and no refill
+//     bookkeeping (v8 spent ~14 VALU per step on its 64-bit window refill);
+//   * a step does kLook lookups in the two-symbol table (LUT2 layout, hpk_code.h), each decoding
+//     up to two codes of <= 12 bits; the second lookup reads the window shifted past the first;
+//   * a step advances <= 24 bits, so it crosses at most one dword: the pair then slides by one
+//     (v_cndmask) and d2 takes d3, the dword read at the top of the step (issued before the table
+//     reads, so it has arrived when they have: no extra wait on the serial chain);
+//   * output: kAcc = false stores each symbol as a byte into the LDS image; kAcc = true gathers a
+//     step's bytes with v_perm and stores whole dwords (fewer LDS stores, more VALU);
+//   * a code longer than 12 bits (EOS included) takes the rarely taken branch: one leading-ones
+//     lookup on a freshly read pair. Bits past a literal's end are never masked: a code that
+//     runs past the end is, by prefix-freeness, longer than what is left whatever follows, so the
+//     walk stops exactly where huffman.rs's bit iterator stops matching (huffman.rs:100-123); the
+//     final padding check (huffman.rs:128-160) looks at the residual bits only;
+//   * long literals (>= 224 encoded bytes: the head of the longest-first queue) are not given to
+//     one lane: a whole wave decodes each of them by self-synchronising speculation (long_decode
+//     below), so a 4 KiB header value no longer holds a fill for thousands of steps.
+#pragma once
+#include "hpk_decode_kernel.h"
+
+namespace hpkdec {
+
+// LDS carve-up: Geo7's regions plus a fifth counter (the long-literal queue head).
+template <int kWaves, int kW, int kO, int kQ>
+struct Geo12 : Geo7<kWaves, kW, kO, kQ, true> {
+    using B = Geo7<kWaves, kW, kO, kQ, true>;
+    static constexpr int kLdsBytes = B::kCtrOff + 32;
+    static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+};
+
+// Longest-first buckets 0..14 hold the literals of >= 224 encoded bytes (lpt_bucket).
+constexpr uint32_t kLongBuckets = 15;
+
+__device__ __forceinline__ void put8(uint8_t* __restrict__ out8, uint32_t pos, uint32_t v, uint32_t oend, int kStore) {
+    if (kStore == kChecked) {
+        if (pos < oend)
+            out8[pos] = (uint8_t)v;
+        else
+            chk_report(1, pos, oend, 0);
+    } else if (kStore == kDword) {
+        out8[pos] = (uint8_t)v;
+    } else {
+        asm volatile("" ::"v"(v));
+    }
+}
+
+__device__ __forceinline__ void put32(uint32_t* __restrict__ out32, uint32_t pos, uint32_t v, uint32_t oend, int kStore) {
+    if (kStore == kChecked) {
+        if (pos < oend)
+            out32[pos] = v;
+        else
+            chk_report(2, pos, oend, 0);
+    } else if (kStore == kDword) {
+        out32[pos] = v;
+    } else {
+        asm volatile("" ::"v"(v));
+    }
+}
+
+// The 32 window bits at bit position p (big-endian dwords).
+__device__ __forceinline__ uint32_t win_at(const uint32_t* __restrict__ win32, uint32_t p) {
+    const uint32_t x = p + 31u;
+    const uint32_t* q = win32 + (x >> 5);
+    return __builtin_amdgcn_alignbit(q[-1], q[0], ~x);
+}
+
+// The codes one table entry decodes with rem bits left: ok1 / ok2 = its first / second code fits
+// inside the literal; returns the bits they use.
+__device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
+    const uint32_t l1 = (e >> 8) & 31u, t1 = (e >> 24) & 31u;
+    ok1 = (e >= HPK_LUT2_ONE) & (l1 <= rem);
+    ok2 = ok1 & (e >= HPK_LUT2_TWO) & (t1 <= rem);
+    return ok2 ? t1 : (ok1 ? l1 : 0u);
+}
+
+// The decoded bytes of an entry, packed little-endian and zero above the g = ok1 + ok2 of them.
+__device__ __forceinline__ uint32_t lut12_bytes(uint32_t e, uint32_t g) {
+    return __builtin_amdgcn_ubfe(__builtin_amdgcn_perm(e, e, 0x0C0C0200u), 0, 8u * g);
+}
+
+// Final status at a stop with rem residual bits and window w there (huffman.rs:128-160): at most
+// 7 residual bits, all ones (the most significant bits of EOS).
+__device__ __forceinline__ uint32_t residual_status(uint32_t rem, uint32_t w) {
+    if (rem == 0) return HPK_OK;
+    if (rem > 7) return HPK_PADDING_TOO_LARGE;
+    return (w | (0xFFFFFFFFu >> rem)) != 0xFFFFFFFFu ? HPK_INVALID_PADDING : HPK_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Lane-per-literal walk.
+
+struct Lit12 {
+    uint32_t X;           // bit position in the window + 31
+    uint32_t Eb;          // end bit position + 31: rem = Eb - X bits left
+    uint32_t d0, d1, d2;  // window dwords (X >> 5) - 1, X >> 5, (X >> 5) + 1
+    uint32_t o;           // next output byte (kAcc: next output dword) in the LDS image
+    uint32_t o0;          // first output byte of the literal (byte stores)
+    uint32_t cnt;         // bytes decoded (kAcc)
+    uint32_t acc, accn;   // pending output bytes and their count 0..3 (kAcc)
+    uint32_t oend;        // checked mode: end of the literal's capacity (bytes / dwords)
+    uint32_t st;          // hpk_status set by the walk (EOS, or padding found by the long-code branch)
+    uint32_t idx;         // literal index in the fill
+    bool prog;            // the last step consumed a code or took the long-code branch
+    bool act;             // holds a fast-path literal not yet finalised
+};
+
+// (Re)load the pair and the next dword at X.
+__device__ __forceinline__ void lit12_load(Lit12& L, const uint32_t* __restrict__ win32) {
+    const uint32_t* p = win32 + (L.X >> 5);
+    L.d0 = p[-1];
+    L.d1 = p[0];
+    L.d2 = p[1];
+}
+
+// Append g (<= 4) bytes p (zero above them) to the pending output; store a dword when one is full.
+template <int kStore>
+__device__ __forceinline__ void acc_push(Lit12& L, uint32_t* __restrict__ out32, uint32_t p, uint32_t g) {
+    const uint64_t x = (uint64_t)p << (8u * L.accn);
+    const uint32_t lo = L.acc | (uint32_t)x;
+    const uint32_t n2 = L.accn + g;  // <= 7
+    const bool full = n2 >= 4u;
+    if (full) put32(out32, L.o, lo, L.oend, kStore);
+    L.o += full ? 1u : 0u;
+    L.acc = full ? (uint32_t)(x >> 32) : lo;
+    L.accn = n2 & 3u;
+    L.cnt += g;
+}
+
+template <int kStore, int kLook, bool kAcc>
+__device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8) {
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
+    const uint32_t d3 = win32[(L.X >> 5) + 2];  // the dword after d2, in case this step crosses one
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t rem = L.Eb - L.X;
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+    bool a1, a2;
+    const uint32_t u1 = lut12(e1, rem, a1, a2);
+    uint32_t use = u1;
+    // a code longer than 12 bits (or EOS) starts here and may still fit
+    bool park = (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);
+    uint32_t pk = 0, g = 0;
+    if (!kAcc) {
+        if (a1) put8(out8, L.o, e1, L.oend, kStore);
+        if (a2) put8(out8, L.o + 1, e1 >> 16, L.oend, kStore);
+        L.o += (uint32_t)a1 + (uint32_t)a2;
+    } else {
+        g = (uint32_t)a1 + (uint32_t)a2;
+        pk = lut12_bytes(e1, g);
+    }
+    if (kLook == 2) {
+        // the first entry was consumed whole: look the next bits up too
+        const bool cont = a1 & (a2 | (e1 < HPK_LUT2_TWO));
+        const uint32_t w2 = w << u1;
+        const uint32_t rem2 = rem - u1;
+        const uint32_t e2 = lut[w2 >> (32 - HPK_LUT_BITS)];
+        bool b1, b2;
+        const uint32_t u2 = lut12(e2, rem2, b1, b2);
+        b1 &= cont;
+        b2 &= cont;
+        if (!kAcc) {
+            if (b1) put8(out8, L.o, e2, L.oend, kStore);
+            if (b2) put8(out8, L.o + 1, e2 >> 16, L.oend, kStore);
+            L.o += (uint32_t)b1 + (uint32_t)b2;
+        } else {
+            const uint32_t g2 = (uint32_t)b1 + (uint32_t)b2;
+            pk |= lut12_bytes(e2, g2) << (8u * g);
+            g += g2;
+        }
+        use += cont ? u2 : 0u;
+        park |= cont & (e2 < HPK_LUT2_ONE) & (rem2 > (uint32_t)HPK_LUT_BITS);
+    }
+    if (kAcc) acc_push<kStore>(L, out32, pk, g);
+    const uint32_t xn = L.X + use;
+    const bool cross = (xn ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xn;
+    L.prog = a1 | park;
+    if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
+        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+        uint32_t s, len;
+        bool eos;
+        lo_decode(wp, lo, s, len, eos);
+        const uint32_t r = L.Eb - L.X;
+        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+            L.st = HPK_PADDING_TOO_LARGE;
+            L.Eb = L.X;
+        } else if (eos) {  // huffman.rs:112-116
+            L.st = HPK_EOS_IN_STRING;
+            L.Eb = L.X;
+        } else {
+            if (kAcc) {
+                acc_push<kStore>(L, out32, s, 1u);
+            } else {
+                put8(out8, L.o, s, L.oend, kStore);
+                L.o += 1;
+            }
+            L.X += len;
+            lit12_load(L, win32);
+        }
+    }
+}
+
+// Final status of a literal whose walk has stopped; a status set by the walk wins.
+__device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
+    if (L.st != HPK_OK) return L.st;
+    return residual_status(L.Eb - L.X, __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X));
+}
+
+// ------------------------------------------------------------------------------------------
+// Wave-cooperative decode of one long literal (self-synchronising speculation).
+//
+// The literal's N bits are cut into 64 segments of S >= 32 bits; lane j walks codes from a start
+// b_j (speculatively j*S) while they start before e_j = (j+1)*S and records where it stops: the
+// first code boundary at or past e_j ("through"), the literal's end, or an EOS. Lane j's true
+// start is lane j-1's stop when that one came through; Huffman walks from a wrong position fall
+// into step with the true one within a few codes, so after one re-walk from the neighbours' stops
+// the starts are all true and a second pass changes nothing. Each round only lanes whose start
+// changed walk again, and the loop ends (lane 0's start is always true, and round r fixes lane r).
+// A final walk writes the symbols at offsets from a scan of the per-lane counts.
+
+enum SegStop : uint32_t { kThrough = 0, kEnded = 1, kEos = 2, kStuck = 3 };
+
+// One lane's walk over [b, e) of a literal at window bit P0 with N bits; writes its symbols to
+// out8[o ...] when kWrite. Returns the stop position; cnt = codes taken, stop = SegStop.
+template <bool kWrite>
+__device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, int kStore,
+                                             uint32_t P0, uint32_t N, uint32_t b, uint32_t e, uint32_t o, uint32_t oend,
+                                             uint32_t& cnt, uint32_t& stop) {
+    uint32_t pos = b;
+    cnt = 0;
+    stop = kThrough;
+    bool run = pos < e;
+    // every pass advances >= 5 bits or stops; the guard only bounds the loop for the compiler and
+    // any unforeseen input (a segment holds <= 8192 bits)
+    for (uint32_t guard = 0; run; ++guard) {
+        if (guard > 4096u) {
+            stop = kStuck;
+            break;
+        }
+        const uint32_t w = win_at(win32, P0 + pos);
+        const uint32_t rem = N - pos;
+        const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+        bool a1, a2;
+        lut12(e1, rem, a1, a2);
+        if (a1) {
+            const uint32_t l1 = (e1 >> 8) & 31u;
+            if (kWrite) put8(out8, o + cnt, e1, oend, kStore);
+            cnt += 1;
+            if (a2 && pos + l1 < e) {  // the second code also starts inside the segment
+                if (kWrite) put8(out8, o + cnt, e1 >> 16, oend, kStore);
+                cnt += 1;
+                pos += (e1 >> 24) & 31u;
+            } else {
+                pos += l1;
+            }
+            run = pos < e;
+        } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
+            uint32_t s, len;
+            bool eos;
+            lo_decode(w, lo, s, len, eos);
+            if (len > rem) {
+                stop = kEnded;
+                run = false;
+            } else if (eos) {
+                stop = kEos;
+                run = false;
+            } else {
+                if (kWrite) put8(out8, o + cnt, s, oend, kStore);
+                cnt += 1;
+                pos += len;
+                run = pos < e;
+            }
+        } else {  // the next code does not fit: the literal ends here
+            stop = kEnded;
+            run = false;
+        }
+    }
+    return pos;
+}
+
+// Whole-wave call (all 64 lanes, wave-uniform arguments): the literal's bits start at window bit
+// P0 (N bits), its output at image byte o0. Returns out_len and the hpk_status.
+template <int kRounds = 64>
+__device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                            const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, int kStore,
+                                            uint32_t P0, uint32_t N, uint32_t o0, uint32_t& out_len, uint32_t& status) {
+    const uint32_t j = threadIdx.x & 63u;
+    const uint32_t S = max(32u, (N + 63u) >> 6);
+    const bool inrange = j * S < N;
+    const uint32_t e = (j + 1) * S;
+    uint32_t b = j * S, cnt = 0, stop = kEnded, pos = b;
+    bool dead = !inrange;
+    if (!dead) pos = seg_walk<false>(win32, lut, lo, out8, kStore, P0, N, b, e, 0, 0, cnt, stop);
+    // round r fixes lane r at the latest, so 64 rounds always suffice
+    bool stuck = false;
+    for (uint32_t round = 0;; ++round) {
+        if (round >= (uint32_t)kRounds) {
+            stuck = kRounds == 64;
+            break;
+        }
+        const uint32_t lpos = __shfl_up(pos, 1);
+        const uint32_t lthrough = __shfl_up((uint32_t)(!dead && stop == kThrough), 1);
+        const uint32_t nb = j == 0 ? 0u : lpos;
+        const bool ndead = !inrange || (j != 0 && !lthrough);
+        const bool changed = ndead != dead || (!ndead && nb != b);
+#ifdef HPK_DEBUG_LONG
+        if (j == 0 && blockIdx.x == 0) printf("N=%u round=%u changed=%llx\n", N, round, (unsigned long long)__ballot(changed));
+#endif
+        if (!__any(changed)) break;
+        if (changed) {
+            b = nb;
+            dead = ndead;
+            if (!dead) {
+                pos = seg_walk<false>(win32, lut, lo, out8, kStore, P0, N, b, e, 0, 0, cnt, stop);
+            } else {
+                pos = b;
+                cnt = 0;
+                stop = kEnded;
+            }
+        }
+    }
+#ifdef HPK_DEBUG_LONG
+    if (j == 0 && blockIdx.x == 0) printf("N=%u rounds done\n", N);
+#endif
+    // output offsets: scan of the live lanes' counts
+    const uint32_t c = dead ? 0u : cnt;
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if (j >= (uint32_t)d) incl += y;
+    }
+    out_len = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // the last live lane holds the literal's end (lane 0 always lives: N > 0)
+    const uint64_t live = __ballot(!dead);
+    const int sl = 63 - __builtin_clzll(live);
+    const uint32_t s_stop = (uint32_t)__builtin_amdgcn_readlane((int)stop, sl);
+    const uint32_t s_pos = (uint32_t)__builtin_amdgcn_readlane((int)pos, sl);
+    status = s_stop == kEos ? (uint32_t)HPK_EOS_IN_STRING : residual_status(N - s_pos, win_at(win32, P0 + s_pos));
+    if (stuck || __any(stop == kStuck)) status = 0x7F;  // never expected: shows up as a bad status
+    if (!dead && c) {
+        uint32_t c2, st2;
+        seg_walk<true>(win32, lut, lo, out8, kStore, P0, N, b, e, o0 + incl - c, o0 + N / 5u, c2, st2);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+
+// kMode: 0 product; diagnostics (never the default): 1 no decode (fill structure only), 2 no
+// output stores, 3 product + per-wave stamps in a.dbg (cycles total / in decode, steps, fills),
+// 4 checked stores (g_chk).
+template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
+          int kCoop = 1>
+__global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
+    using G = Geo12<kWaves, kW, kO, kQ>;
+    constexpr int R = G::kMetaRounds, S = G::kStageRounds;
+    constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
+    static_assert(kChunk >= 64, "a refill can hand out 64 slots");
+    unsigned long long t_start = 0, t_dec = 0, n_steps = 0, n_fills = 0;
+    if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
+    __shared__ __attribute__((aligned(16))) uint8_t smem[G::kLdsBytes];
+    uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
+    uint32_t* s_lut = reinterpret_cast<uint32_t*>(smem + G::kLutOff);
+    uint8_t* s_in = smem + G::kInOff;
+    const uint32_t* win32 = reinterpret_cast<const uint32_t*>(s_in);
+    uint8_t* s_out = smem + G::kOutOff;
+    uint32_t* s_out32 = reinterpret_cast<uint32_t*>(s_out);
+    uint2* s_q = reinterpret_cast<uint2*>(smem + G::kQOff);
+    uint32_t* s_lenst = reinterpret_cast<uint32_t*>(smem + G::kLenOff);  // len | status << 24
+    uint32_t* s_hist = reinterpret_cast<uint32_t*>(smem + G::kHistOff);
+    uint32_t* s_bbase = s_hist + 64;
+    // [0] fitting count, [1] lane-queue head, [2] input end of the fill, [3] output end of the
+    // fill, [4] long-queue head
+    uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);
+    for (uint32_t t = threadIdx.x; t < kLoBytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+    for (uint32_t t = threadIdx.x; t < (uint32_t)G::kLutBytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut2)[t];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
+    const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+    const uint32_t in_end = a.in_off[a.n] + a.in_mis;
+    const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
+    // last chunk holding a byte of THIS workgroup's literals: windows never read past it
+    const uint32_t r_end = a.in_off[BB] + a.in_mis;
+    const uint32_t rlast16 = r_end ? (r_end - 1) >> 4 : 0;
+
+    // write back one decoded fill from the LDS image: the output span [G0, G1) with 16-byte
+    // stores (bytewise in the two end chunks, which neighbours own), then out_len and status
+    auto flush = [&](uint32_t fcur, uint32_t fk, uint32_t G0, uint32_t G1) {
+        const uint32_t ob = G0 & ~15u;
+        if (kMode != 2) {
+            const uint32_t c0 = ob >> 4, c1 = (G1 + 15) >> 4;
+            const uint4* l16 = reinterpret_cast<const uint4*>(s_out);
+            uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
+#pragma unroll
+            for (int r = 0; r < G::kFlushRounds; ++r) {
+                const uint32_t ci = c0 + tid + (uint32_t)G::kBlock * r;
+                if (ci < c1 && (ci << 4) >= G0 && (ci << 4) + 16u <= G1) g16[ci] = l16[ci - c0];
+            }
+            if (tid < 2) {  // the partial chunks at the two ends
+                const uint32_t g = tid == 0 ? c0 << 4 : (c1 - 1) << 4;
+                if (!(g >= G0 && g + 16u <= G1) && (tid == 0 || c1 - 1 != c0)) {
+#pragma unroll 1
+                    for (uint32_t b = 0; b < 16u; ++b)
+                        if (g + b >= G0 && g + b < G1) a.out_base[g + b] = s_out[g + b - ob];
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = tid + (uint32_t)G::kBlock * r;
+            if (i < fk) {
+                const uint32_t v = s_lenst[i];
+                a.out_len[fcur + i] = v & 0xFFFFFFu;
+                a.status[fcur + i] = (uint8_t)(v >> 24);
+            }
+        }
+    };
+    uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
+
+    uint32_t cur = BA;
+    uint32_t gin = 0, gout = 0;  // exact input / output start of the fill (blob-relative + mis)
+    Prefetch<R, S> P;
+    if (cur < BB) {
+        gin = a.in_off[cur] + a.in_mis;
+        gout = a.out_off[cur] + a.out_mis;
+        prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
+    }
+    while (cur < BB) {  // block-uniform
+        const uint32_t cntl = min((uint32_t)kQ, BB - cur);
+        const uint32_t base16 = gin & ~15u;
+        const uint32_t ob16 = gout & ~15u;
+        lds_barrier();  // previous fill decoded and its image read out: every LDS region is free
+        if (tid < 64) s_hist[tid] = 0;
+        if (tid == 0) {
+            s_ctr[0] = 0;
+            s_ctr[1] = G::kBlock;  // lane-queue slots handed out at the start
+            s_ctr[2] = gin;
+            s_ctr[3] = gout;
+            s_ctr[4] = 0;
+        }
+        lds_barrier();
+        uint32_t ex[R], ey[R], pos[R];
+        uint32_t kw = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
+            const uint32_t o0 = P.oo0[r] + a.out_mis, o1 = P.oo1[r] + a.out_mis;
+            // fitting literals form a prefix (offsets are non-decreasing)
+            const bool fits = t < cntl && p1 - base16 <= (uint32_t)kW && o1 - ob16 <= (uint32_t)kO;
+            pos[r] = 0xFFFFFFFFu;
+            if (fits) {
+                const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
+                // fast path: a region holding hpk_decoded_bound(nbytes) bytes (dword-aligned in
+                // start and size for the dword stores, which write up to 3 bytes past the end)
+                const bool fast = ocap >= (nbytes * 8u) / 5u && (!kAcc || ((o0 | ocap) & 3u) == 0);
+                ex[r] = (p0 - base16) | (nbytes << 16);
+                ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
+                const uint32_t bk = lpt_bucket(nbytes);
+                pos[r] = (bk << 16) | atomicAdd(&s_hist[bk], 1u);
+            }
+            const uint64_t fb = __ballot(fits);
+            kw += (uint32_t)__popcll(fb);
+            if (fb) {  // the wave's last fitting literal ends furthest (offsets non-decreasing)
+                const int hl = 63 - __builtin_clzll(fb);
+                const uint32_t e_in = (uint32_t)__builtin_amdgcn_readlane((int)p1, hl);
+                const uint32_t e_out = (uint32_t)__builtin_amdgcn_readlane((int)o1, hl);
+                if (lane == 0) {
+                    atomicMax(&s_ctr[2], e_in);
+                    atomicMax(&s_ctr[3], e_out);
+                }
+            }
+        }
+        if (lane == 0 && kw) atomicAdd(&s_ctr[0], kw);
+        lds_barrier();
+        const uint32_t k = s_ctr[0];
+        if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global
+            if (tid == 0) {
+                const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), last16 * 4 + 3};
+                uint8_t* dst = a.out_base + gout;
+                Lit L = {};
+                lit_bytes_to(L, g, s_lo, [&](uint32_t j, uint8_t v) { dst[j] = v; },
+                             a.out_off[cur + 1] - a.out_off[cur], gin, a.in_off[cur + 1] + a.in_mis - gin);
+                a.out_len[cur] = L.cnt;
+                a.status[cur] = (uint8_t)lit_status(L);
+            }
+            cur += 1;
+            if (cur < BB) {
+                gin = a.in_off[cur] + a.in_mis;
+                gout = a.out_off[cur] + a.out_mis;
+                prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
+            }
+            continue;
+        }
+        const uint32_t gin_next = s_ctr[2], gout_next = s_ctr[3];  // = in/out offsets of cur + k
+        // bucket bases (exclusive scan over 64 buckets by wave 0), then scatter the entries
+        if (tid < 64) {
+            const uint32_t v = s_hist[tid];
+            uint32_t x = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= (uint32_t)d) x += y;
+            }
+            s_bbase[tid] = x - v;
+        }
+        // the window, from the prefetched registers, as big-endian dwords: bit P of the stream
+        // is bit 31 - P % 32 of dword P / 32
+        {
+            uint4* l16 = reinterpret_cast<uint4*>(s_in);
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                const uint4 c = P.chunk[r];
+                if (tid + G::kBlock * r < kW / 16)
+                    l16[tid + G::kBlock * r] = make_uint4(__builtin_bswap32(c.x), __builtin_bswap32(c.y),
+                                                          __builtin_bswap32(c.z), __builtin_bswap32(c.w));
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (pos[r] != 0xFFFFFFFFu) s_q[s_bbase[pos[r] >> 16] + (pos[r] & 0xFFFFu)] = make_uint2(ex[r], ey[r]);
+        const uint32_t nlong = kCoop ? s_bbase[kLongBuckets] : 0u;  // the queue's head: literals of >= 224 bytes
+        // the next fill's offsets and window: in flight during this fill's decode. Unconditional
+        // (clamped past the range end), so no register phi forces a wait on the stores below.
+        const uint32_t cur_next = cur + k;
+        {
+            const uint32_t c = min(cur_next, BB - 1);
+            prefetch_fill<G::kBlock>(P, a, tid, c, min(c + (uint32_t)kQ, BB), gin_next & ~15u, rlast16);
+        }
+        // the previous fill's write-back: its image is read out before this fill decodes over it
+        if (pk) flush(pcur, pk, pG0, pG1);
+        pk = k;
+        pcur = cur;
+        pG0 = gout;
+        pG1 = gout_next;
+        lds_barrier();
+        unsigned long long td0 = 0;
+        if (kMode == 3) {
+            td0 = __builtin_amdgcn_s_memtime();
+            n_fills += 1;
+        }
+        if (kMode == 1) {  // diagnostic: no decode; lengths from the queue keep the fill live
+            for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
+                const uint2 e = s_q[tt];
+                s_lenst[e.y & 0xFFFu] = (e.x >> 16) + s_in[e.x & 0xFFFFu];
+            }
+        }
+        // long literals first (longest-first): one wave each, round-robin over the queue's head.
+        // Everything in this loop is wave-uniform and held in scalar registers: with a lane-0
+        // atomic or a branch on a vector value the compiler makes the loop divergent, and the
+        // cross-lane operations inside long_decode then run under a partial exec mask.
+        if (kMode != 1 && nlong) {
+            const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+            for (uint32_t jl = wv; jl < nlong; jl += kWaves) {
+                const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].x);
+                const uint32_t ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].y);
+                if (ey & kQ7Byte) continue;  // capacity below the bound: the byte pass below
+                uint32_t len = 0, st = 0;
+                if (kCoop == 3)
+                    long_decode<0>(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
+                                   (ey >> 12) & 0x1FFFFu, len, st);
+                if (kCoop == 1)
+                    long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
+                                (ey >> 12) & 0x1FFFFu, len, st);
+                if (lane == 0) s_lenst[ey & 0xFFFu] = len | (st << 24);
+            }
+        }
+        const uint32_t kl = k - nlong;  // lane-queue entries s_q[nlong, k)
+        if (kMode != 1 && kl) {
+            const uint2* lq = s_q + nlong;
+            Lit12 L;
+            uint32_t t = tid;
+            uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
+            // Branch-free (re)start: lanes past the queue read a clamped entry and stay idle (no
+            // bits: rem = 0). The loop has no divergent exits, so the ballots see the whole wave.
+            auto begin = [&](uint32_t tt) {
+                const uint2 e = lq[min(tt, kl - 1)];
+                L.act = tt < kl && !(e.y & kQ7Byte);
+                L.idx = e.y & 0xFFFu;
+                const uint32_t nb = e.x >> 16;
+                const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
+                L.X = (e.x & 0xFFFFu) * 8u + 31u;
+                L.Eb = L.X + (L.act ? nb * 8u : 0u);
+                L.o = kAcc ? ob >> 2 : ob;
+                L.o0 = ob;
+                L.oend = kAcc ? (ob + nb * 8u / 5u + 3u) >> 2 : ob + nb * 8u / 5u;
+                L.cnt = 0;
+                L.acc = 0;
+                L.accn = 0;
+                L.st = HPK_OK;
+                L.prog = false;
+                lit12_load(L, win32);
+            };
+            begin(t);
+            for (;;) {
+#pragma unroll
+                for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out);
+                if (kMode == 3) n_steps += kRefillN;
+                const bool fin = t < kl && !L.prog;
+                if (__any(fin)) {
+                    if (fin && L.act) {
+                        if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
+                        s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+                    }
+                    const bool free_lane = fin || t >= kl;
+                    const uint64_t fm = __ballot(free_lane);
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+                    // free lanes take the wave's reserved slots [qb, qe) in rank order; when those
+                    // run short the wave reserves kChunk more with one LDS atomic
+                    const uint32_t need = (uint32_t)__popcll(fm), have = qe - qb;
+                    uint32_t base = qb + rank;
+                    if (have < need) {  // wave-uniform
+                        uint32_t nb = 0;
+                        if (rank == 0 && free_lane) nb = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
+                        nb = (uint32_t)__builtin_amdgcn_readlane((int)nb, (int)__builtin_ctzll(fm));
+                        if (rank >= have) base = nb + (rank - have);
+                        qb = nb + (need - have);
+                        qe = nb + kChunk;
+                    } else {
+                        qb += need;
+                    }
+                    qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
+                    qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
+                    if (free_lane) {
+                        t = base;
+                        begin(base);
+                    }
+                }
+                if (!__any(t < kl)) break;
+            }
+        }
+        if (kMode == 3) t_dec += __builtin_amdgcn_s_memtime() - td0;
+        // literals whose output region is below the decoded bound (or not dword-aligned for the
+        // dword stores): byte stores into the image with a capacity check per byte
+        for (uint32_t tt = tid; kMode != 1 && tt < k; tt += G::kBlock) {
+            const uint2 e = s_q[tt];
+            if (e.y & kQ7Byte) {
+                const uint32_t i = e.y & 0xFFFu;
+                const uint32_t o = a.out_off[cur + i] + a.out_mis - ob16;
+                Lit B = {};
+                lit_bytes_to(B, LdsSwapSrc{win32}, s_lo, [&](uint32_t j, uint8_t v) { s_out[o + j] = v; },
+                             a.out_off[cur + i + 1] - a.out_off[cur + i], e.x & 0xFFFFu, e.x >> 16);
+                s_lenst[i] = B.cnt | (lit_status(B) << 24);
+            }
+        }
+        cur = cur_next;
+        gin = gin_next;
+        gout = gout_next;
+    }
+    if (pk) {
+        lds_barrier();
+        flush(pcur, pk, pG0, pG1);
+    }
+    if (kMode == 3 && lane == 0) {
+        const uint64_t gwi = (uint64_t)blockIdx.x * kWaves + (tid >> 6);
+        a.dbg[gwi * 4 + 0] = __builtin_amdgcn_s_memtime() - t_start;
+        a.dbg[gwi * 4 + 1] = t_dec;
+        a.dbg[gwi * 4 + 2] = n_steps;
+        a.dbg[gwi * 4 + 3] = n_fills;
+    }
+}
+
+}  // namespace hpkdec

@@ -26,6 +26,7 @@ struct DecodeArgs {
     const uint8_t* t8;
     const uint16_t* lo;
     const uint32_t* lut;  // two-symbol table (hpk_code.h), step 8
+    const uint32_t* lut2; // the same in the LUT2 layout (decode v12)
     unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
 };
 

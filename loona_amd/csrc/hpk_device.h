@@ -15,6 +15,7 @@ struct hpk_ctx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     uint32_t* d_lut = nullptr;
+    uint32_t* d_lut2 = nullptr;
     uint16_t* d_lo = nullptr;
     uint8_t* d_t8 = nullptr;
     uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length

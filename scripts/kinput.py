@@ -11,7 +11,15 @@ from loona_amd import synth  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
 path = sys.argv[2] if len(sys.argv) > 2 else "/tmp/kin.bin"
 n = int(sys.argv[3]) if len(sys.argv) > 3 else None
-w = getattr(synth, cfg)() if n is None else getattr(synth, cfg)(n=n)
+if cfg.startswith("interop"):  # the interop corpus' Huffman literals (interop_long: >= 224 B only)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    from hpk_util import interop_literals, pack  # noqa: E402
+
+    lits = [x for x in interop_literals() if cfg == "interop" or len(x) >= 224]
+    blob, off = pack(lits * (n or 1))
+    w = synth.Workload(cfg, blob, off)
+else:
+    w = getattr(synth, cfg)() if n is None else getattr(synth, cfg)(n=n)
 with open(path, "wb") as f:
     np.array([w.n, w.enc_bytes], np.uint32).tofile(f)
     w.enc_off.astype(np.uint32).tofile(f)

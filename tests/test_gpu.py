@@ -95,6 +95,45 @@ def test_random_and_edge_literals(codec):
     compare_batches(gpu_decode(codec, blob, off), oracle_decode_batch(blob, off), "random")
 
 
+def test_long_literals(codec):
+    """Literals of >= 224 encoded bytes take the wave-cooperative (self-synchronising) path: valid
+    ones of every code length, random bytes (padding errors), an EOS in the middle at every bit
+    offset class, bad padding after a long valid run, and long runs of 30-bit codes and of ones
+    (where speculative starts synchronise late). Bit-exact against the oracle, with short literals
+    interleaved so both paths run in the same fills."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(2025)
+    lits = []
+    for n in rng.integers(224, 4000, size=300):  # valid, mixed alphabets
+        s = rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() if rng.random() < 0.5 else \
+            rng.choice(np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;, ", np.uint8), int(n)).tobytes()
+        lits.append(huffman_encode(s))
+        lits.append(rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8).tobytes())
+    for n in rng.integers(224, 3000, size=200):  # random bytes
+        lits.append(rng.integers(0, 256, int(n), dtype=np.uint8).tobytes())
+    eos = (1 << 30) - 1
+    for k in range(64):  # EOS after a long valid prefix, at every offset mod 64 bits
+        body = huffman_encode(b"x" * (300 + k))
+        bits = int.from_bytes(body, "big") >> (len(body) * 8 - (300 + k) * 7)  # 'x' is 7 bits
+        nb = (300 + k) * 7
+        tail = int(rng.integers(0, 1 << 20))
+        v = (((bits << 30) | eos) << 20) | tail
+        tot = nb + 50
+        pad = (-tot) % 8
+        lits.append(((v << pad) | ((1 << pad) - 1)).to_bytes((tot + pad) // 8, "big"))
+    for k in range(32):  # long valid run then a bad padding / too much padding
+        body = bytearray(huffman_encode(b"accept-encoding: gzip, deflate" * (10 + k)))
+        body[-1] &= 0xF0
+        lits.append(bytes(body))
+        lits.append(huffman_encode(b"y" * (400 + k)) + b"\xff")
+    lits.append(b"\xff" * 3000)  # ones only: EOS at once
+    lits.append(huffman_encode(bytes([1]) * 800))  # 23-bit codes back to back
+    lits.append(huffman_encode(bytes(range(256)) * 12))  # every code length
+    blob, off = pack(lits)
+    compare_batches(gpu_decode(codec, blob, off), oracle_decode_batch(blob, off), "long literals")
+
+
 def test_empty_batch_and_empty_literals(codec):
     blob, off = pack([])
     got = gpu_decode(codec, blob, off)
