@@ -210,8 +210,6 @@ int main(int argc, char** argv) {
     if (argc > 3) {  // one named variant per process (a hang then names itself)
         g_only = argv[3];
         run12<0, 3, 2, false, 16, 40960, 79104, 2048, 0>("coop0", d, ref_len, ref_st, ref_out, cu, iters);
-        run12<0, 3, 2, false, 16, 40960, 79104, 2048, 2>("coop2", d, ref_len, ref_st, ref_out, cu, iters);
-        run12<0, 3, 2, false, 16, 40960, 79104, 2048, 3>("coop3", d, ref_len, ref_st, ref_out, cu, iters);
         run12<4, 3, 2, false>("coop1_checked", d, ref_len, ref_st, ref_out, cu, 1);
         run12<0, 3, 2, false>("coop1", d, ref_len, ref_st, ref_out, cu, iters);
         return 0;

@@ -41,7 +41,7 @@ using namespace hpkdec;
 // byte stores into the image (bench/kvariants: profiles/r01/kvariants_v12*.jsonl).
 constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 3, kChunk = 64, kLook = 2;
 constexpr bool kAcc = false;
-constexpr int kCoop = 0;  // cooperative long-literal path: off until it is validated on the GPU
+constexpr int kCoop = 1;  // literals of >= 224 encoded bytes: one wave each (self-synchronising walk)
 using Geo = Geo12<kWaves, kW, kO, kQ>;
 #define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop>
 

@@ -293,7 +293,6 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
 
 // Whole-wave call (all 64 lanes, wave-uniform arguments): the literal's bits start at window bit
 // P0 (N bits), its output at image byte o0. Returns out_len and the hpk_status.
-template <int kRounds = 64>
 __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, int kStore,
                                             uint32_t P0, uint32_t N, uint32_t o0, uint32_t& out_len, uint32_t& status) {
@@ -307,8 +306,8 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
     // round r fixes lane r at the latest, so 64 rounds always suffice
     bool stuck = false;
     for (uint32_t round = 0;; ++round) {
-        if (round >= (uint32_t)kRounds) {
-            stuck = kRounds == 64;
+        if (round > 64u) {
+            stuck = true;
             break;
         }
         const uint32_t lpos = __shfl_up(pos, 1);
@@ -316,9 +315,6 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
         const uint32_t nb = j == 0 ? 0u : lpos;
         const bool ndead = !inrange || (j != 0 && !lthrough);
         const bool changed = ndead != dead || (!ndead && nb != b);
-#ifdef HPK_DEBUG_LONG
-        if (j == 0 && blockIdx.x == 0) printf("N=%u round=%u changed=%llx\n", N, round, (unsigned long long)__ballot(changed));
-#endif
         if (!__any(changed)) break;
         if (changed) {
             b = nb;
@@ -332,9 +328,6 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
             }
         }
     }
-#ifdef HPK_DEBUG_LONG
-    if (j == 0 && blockIdx.x == 0) printf("N=%u rounds done\n", N);
-#endif
     // output offsets: scan of the live lanes' counts
     const uint32_t c = dead ? 0u : cnt;
     uint32_t incl = c;
@@ -362,6 +355,7 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // kMode: 0 product; diagnostics (never the default): 1 no decode (fill structure only), 2 no
 // output stores, 3 product + per-wave stamps in a.dbg (cycles total / in decode, steps, fills),
 // 4 checked stores (g_chk).
+// kCoop: 1 = long literals by whole waves (product), 0 = every literal by one lane (comparison).
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
           int kCoop = 1>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
@@ -573,13 +567,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].x);
                 const uint32_t ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].y);
                 if (ey & kQ7Byte) continue;  // capacity below the bound: the byte pass below
-                uint32_t len = 0, st = 0;
-                if (kCoop == 3)
-                    long_decode<0>(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
-                                   (ey >> 12) & 0x1FFFFu, len, st);
-                if (kCoop == 1)
-                    long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
-                                (ey >> 12) & 0x1FFFFu, len, st);
+                uint32_t len, st;
+                long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
+                            (ey >> 12) & 0x1FFFFu, len, st);
                 if (lane == 0) s_lenst[ey & 0xFFFu] = len | (st << 24);
             }
         }
