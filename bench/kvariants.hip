@@ -103,17 +103,17 @@ static void run11(const char* name, Dev& d, const std::vector<uint32_t>& ref_len
 static const char* g_only = nullptr;  // run only the variant of this name (argv[3])
 
 template <int kMode, int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048,
-          int kCoop = 1>
+          int kCoop = 1, int kBlocksPerCu = 1, int kSched = 0>
 static void run12(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                   const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
     if (g_only && strcmp(g_only, name) != 0) return;
     using G = Geo12<kWaves, kW, kO, kQ>;
-    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop>, 0, G::kBlock, 1, d,
-                  ref_len, ref_st, ref_out, num_cu, iters);
+    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched>, 0, G::kBlock, kBlocksPerCu,
+                  d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
 // v12 diagnostic stamps (kMode 3): per wave total cycles, cycles in the decode phases, steps, fills
-template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048>
+template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048, int kSched = 0>
 static void stamps12(const char* name, Dev& d, int num_cu) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     const size_t nw = (size_t)num_cu * kWaves;
@@ -121,7 +121,7 @@ static void stamps12(const char* name, Dev& d, int num_cu) {
     CK(hipMalloc(&dbg, nw * 4 * 8));
     DecodeArgs a = d.a;
     a.dbg = dbg;
-    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc>;
+    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, 1, kSched>;
     for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(num_cu), dim3(G::kBlock), 0, 0, a);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nw * 4);
@@ -133,7 +133,7 @@ static void stamps12(const char* name, Dev& d, int num_cu) {
             mx[j] = std::max(mx[j], (double)h[w * 4 + j]);
         }
     printf("{\"stamps\": \"%s\", \"cycles_mean\": %.0f, \"cycles_max\": %.0f, \"decode_cycles_mean\": %.0f, "
-           "\"decode_cycles_max\": %.0f, \"steps_mean\": %.1f, \"steps_max\": %.0f, \"fills_mean\": %.2f}\n",
+           "\"decode_cycles_max\": %.0f, \"steps_mean\": %.1f, \"steps_max\": %.0f, \"barrier_wait_mean\": %.0f}\n",
            name, s[0] / nw, mx[0], s[1] / nw, mx[1], s[2] / nw, mx[2], s[3] / nw);
     fflush(stdout);
     CK(hipFree(dbg));
@@ -214,8 +214,8 @@ int main(int argc, char** argv) {
         run12<0, 3, 2, false>("coop1", d, ref_len, ref_st, ref_out, cu, iters);
         return 0;
     }
-    run7<0, 16, 40960, 79104, 2048, 6, 64, 8>("v8_r6", d, ref_len, ref_st, ref_out, cu, iters);
-    run12<0, 3, 2, false>("v12_l2b_r3", d, ref_len, ref_st, ref_out, cu, iters);
-    run12<0, 3, 2, true>("v12_l2a_r3", d, ref_len, ref_st, ref_out, cu, iters);
+    run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("v13_snake_r2", d, ref_len, ref_st, ref_out, cu, iters);
+    run12<0, 2, 2, true, 16, 40960, 79104, 2048, 1, 1, 1>("v13_snake_acc_r2", d, ref_len, ref_st, ref_out, cu, iters);
+    run12<2, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("v13_snake_r2_nostore", d, ref_len, ref_st, ref_out, cu, iters);
     return 0;
 }

@@ -4,7 +4,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.12 gfx950 decode v12 (alignbit bit-position step, two lookups per step, cooperative long literals, LDS image, longest-first queue)"
+#define HPK_VERSION "hpk 0.13 gfx950 decode v13 (alignbit step, two lookups per step, static snake schedule, cooperative long literals, LDS image)"
 
 static thread_local std::string t_last_error;
 

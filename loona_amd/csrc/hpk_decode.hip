@@ -16,9 +16,10 @@
 //   * literals of >= 224 encoded bytes (the queue's head) are decoded one per wave, cooperatively:
 //     64 lanes walk 64 segments from speculative starts and re-walk from their neighbours' true
 //     stops until nothing changes (Huffman walks resynchronise within a few codes);
-//   * the other literals are decoded one per lane out of LDS; free lanes take the next queue
-//     slots every 3 steps (ballot + mbcnt) from a per-wave reservation topped up 64 slots at a time
-//     with one LDS atomic, so waves the SIMD's age-priority arbitration favours take more literals;
+//   * the other literals are decoded one per lane out of LDS in a static snake over the
+//     longest-first queue: lane i takes slots i and 2*1024-1-i (the longest with the shortest),
+//     the second literal's entry and first window dwords read while the first one decodes, so a
+//     lane moves on without waiting for LDS;
 //   * a step is two lookups in the 12-bit two-symbol table, each decoding up to two codes of
 //     <= 12 bits, from a 32-bit window made by ONE v_alignbit out of a register-held dword pair;
 //     a code longer than 12 bits (or EOS) takes one leading-ones lookup (any code in one read).
@@ -37,13 +38,13 @@ using namespace hpkdec;
 
 // Product geometry (v12): 16 waves (one 1024-thread workgroup) per CU; per fill a 40 KiB input
 // window, a 77 KiB output image and a 2048-entry longest-first queue, plus the 16 KiB two-symbol
-// table; two lookups per step, lanes refill every 3 steps, waves reserve 64 queue slots at a time,
-// byte stores into the image (bench/kvariants: profiles/r01/kvariants_v12*.jsonl).
-constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 3, kChunk = 64, kLook = 2;
+// table; two lookups per step, lanes check for a finished literal every 2 steps, static snake
+// schedule, byte stores into the image (bench/kvariants: profiles/r01/kvariants_v1[23]*.jsonl).
+constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2, kChunk = 64, kLook = 2, kSched = 1;
 constexpr bool kAcc = false;
 constexpr int kCoop = 1;  // literals of >= 224 encoded bytes: one wave each (self-synchronising walk)
 using Geo = Geo12<kWaves, kW, kO, kQ>;
-#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop>
+#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched>
 
 static int g_debug_mode = -1;
 

@@ -353,11 +353,15 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // ------------------------------------------------------------------------------------------
 
 // kMode: 0 product; diagnostics (never the default): 1 no decode (fill structure only), 2 no
-// output stores, 3 product + per-wave stamps in a.dbg (cycles total / in decode, steps, fills),
+// output stores, 3 product + per-wave stamps in a.dbg (cycles: total, in the decode loops,
+// steps, waiting at the fill-top barrier),
 // 4 checked stores (g_chk).
 // kCoop: 1 = long literals by whole waves (product), 0 = every literal by one lane (comparison).
+// kSched: 0 = lanes take queue slots dynamically (ballot + per-wave reservations), 1 = static
+// snake: lane i decodes slots i and 2*block-1-i of the longest-first queue, the second one's
+// entry and window dwords prefetched while the first decodes (no refill stall).
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
-          int kCoop = 1>
+          int kCoop = 1, int kSched = 0>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -407,13 +411,11 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 const uint32_t ci = c0 + tid + (uint32_t)G::kBlock * r;
                 if (ci < c1 && (ci << 4) >= G0 && (ci << 4) + 16u <= G1) g16[ci] = l16[ci - c0];
             }
-            if (tid < 2) {  // the partial chunks at the two ends
-                const uint32_t g = tid == 0 ? c0 << 4 : (c1 - 1) << 4;
-                if (!(g >= G0 && g + 16u <= G1) && (tid == 0 || c1 - 1 != c0)) {
-#pragma unroll 1
-                    for (uint32_t b = 0; b < 16u; ++b)
-                        if (g + b >= G0 && g + b < G1) a.out_base[g + b] = s_out[g + b - ob];
-                }
+            if (tid < 32) {  // the partial chunks at the two ends, one byte per lane
+                const uint32_t g = tid < 16 ? c0 << 4 : (c1 - 1) << 4;
+                const bool partial = !(g >= G0 && g + 16u <= G1) && (tid < 16 || c1 - 1 != c0);
+                const uint32_t x = g + (tid & 15u);
+                if (partial && x >= G0 && x < G1) a.out_base[x] = s_out[x - ob];
             }
         }
 #pragma unroll
@@ -440,7 +442,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         const uint32_t cntl = min((uint32_t)kQ, BB - cur);
         const uint32_t base16 = gin & ~15u;
         const uint32_t ob16 = gout & ~15u;
+        unsigned long long tb0 = 0;
+        if (kMode == 3) tb0 = __builtin_amdgcn_s_memtime();
         lds_barrier();  // previous fill decoded and its image read out: every LDS region is free
+        if (kMode == 3) n_fills += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: barrier wait)
         if (tid < 64) s_hist[tid] = 0;
         if (tid == 0) {
             s_ctr[0] = 0;
@@ -547,10 +552,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         pG1 = gout_next;
         lds_barrier();
         unsigned long long td0 = 0;
-        if (kMode == 3) {
-            td0 = __builtin_amdgcn_s_memtime();
-            n_fills += 1;
-        }
+        if (kMode == 3) td0 = __builtin_amdgcn_s_memtime();
         if (kMode == 1) {  // diagnostic: no decode; lengths from the queue keep the fill live
             for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
                 const uint2 e = s_q[tt];
@@ -574,7 +576,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
         const uint32_t kl = k - nlong;  // lane-queue entries s_q[nlong, k)
-        if (kMode != 1 && kl) {
+        if (kMode != 1 && kl && kSched == 0) {
             const uint2* lq = s_q + nlong;
             Lit12 L;
             uint32_t t = tid;
@@ -636,6 +638,54 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     }
                 }
                 if (!__any(t < kl)) break;
+            }
+        }
+        if (kMode != 1 && kl && kSched == 1) {
+            static_assert(kSched != 1 || kQ <= 2 * G::kBlock, "static snake: two literals per lane at most");
+            const uint2* lq = s_q + nlong;
+            Lit12 L, N;  // the literal being decoded and the lane's next one (prefetched)
+            auto load = [&](Lit12& T, uint32_t tt) {
+                const uint2 e = lq[min(tt, kl - 1)];
+                T.act = tt < kl && !(e.y & kQ7Byte);
+                T.idx = e.y & 0xFFFu;
+                const uint32_t nb = e.x >> 16;
+                const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
+                T.X = (e.x & 0xFFFFu) * 8u + 31u;
+                T.Eb = T.X + (T.act ? nb * 8u : 0u);
+                T.o = kAcc ? ob >> 2 : ob;
+                T.o0 = ob;
+                T.oend = kAcc ? (ob + nb * 8u / 5u + 3u) >> 2 : ob + nb * 8u / 5u;
+                T.cnt = 0;
+                T.acc = 0;
+                T.accn = 0;
+                T.st = HPK_OK;
+                T.prog = false;
+                lit12_load(T, win32);
+            };
+            load(L, tid);
+            const uint32_t t2 = 2u * G::kBlock - 1u - tid;
+            bool nv = t2 < kl;  // a second literal is waiting in N
+            load(N, t2);
+            for (;;) {
+#pragma unroll
+                for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out);
+                if (kMode == 3) n_steps += kRefillN;
+                const bool fin = !L.prog;  // no progress in the last step: finished (or idle)
+                if (__any(fin)) {
+                    if (fin && L.act) {
+                        if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
+                        s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+                    }
+                    if (fin) {
+                        if (nv) {
+                            L = N;
+                            nv = false;
+                        } else {
+                            L.act = false;
+                        }
+                    }
+                }
+                if (!__any(L.act || nv)) break;
             }
         }
         if (kMode == 3) t_dec += __builtin_amdgcn_s_memtime() - td0;
