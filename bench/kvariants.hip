@@ -212,6 +212,11 @@ int main(int argc, char** argv) {
         run12<0, 3, 2, false, 16, 40960, 79104, 2048, 0>("coop0", d, ref_len, ref_st, ref_out, cu, iters);
         run12<4, 3, 2, false>("coop1_checked", d, ref_len, ref_st, ref_out, cu, 1);
         run12<0, 3, 2, false>("coop1", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("coop1_snake", d, ref_len, ref_st, ref_out, cu, iters);
+        if (!strcmp(g_only, "stamps")) {
+            stamps12<2, 2, false, 16, 40960, 79104, 2048, 1>("coop1_snake", d, cu);
+            stamps12<3, 2, false>("coop1", d, cu);
+        }
         return 0;
     }
     run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("v13_snake_r2", d, ref_len, ref_st, ref_out, cu, iters);

@@ -291,45 +291,132 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
     return pos;
 }
 
+// A lane's walk state in long_decode: where it stopped, how it stopped, the codes it took, and a
+// mask of the code starts it passed in the first 64 bits of its segment.
+struct SegWalk {
+    uint32_t pos, cnt, stop;
+    uint64_t mask;  // bit i: a code started at segment start + i
+};
+
+// seg_walk without output, recording code starts in [s0, s0 + 64). With kResume, the walk from b
+// stops at the first code start that `old` also passed: from there on the old walk is valid (same
+// bits, same boundaries), so its counts, stop and mask are spliced in. A re-walk from a corrected
+// start therefore costs the few codes until the two walks fall into step, not the segment.
+template <bool kResume>
+__device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                              const uint16_t* __restrict__ lo, uint32_t P0, uint32_t N, uint32_t s0,
+                                              uint32_t b, uint32_t e, const SegWalk& old) {
+    SegWalk r = {b, 0u, (uint32_t)kThrough, 0ull};
+    // at a code start p: true when the walk joins `old` there (r completed from old)
+    auto join = [&](uint32_t p) {
+        const uint32_t i = p - s0;
+        if (i >= 64u) return false;
+        const uint64_t bit = 1ull << i;
+        if (kResume && (old.mask & bit)) {
+            r.cnt += old.cnt - (uint32_t)__popcll(old.mask & (bit - 1));
+            r.mask |= old.mask & ~(bit - 1);
+            r.pos = old.pos;
+            r.stop = old.stop;
+            return true;
+        }
+        r.mask |= bit;
+        return false;
+    };
+    bool run = r.pos < e;
+    for (uint32_t guard = 0; run; ++guard) {
+        if (guard > 4096u) {
+            r.stop = kStuck;
+            break;
+        }
+        if (join(r.pos)) break;
+        const uint32_t pos = r.pos;
+        const uint32_t w = win_at(win32, P0 + pos);
+        const uint32_t rem = N - pos;
+        const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+        bool a1, a2;
+        lut12(e1, rem, a1, a2);
+        if (a1) {
+            const uint32_t p2 = pos + ((e1 >> 8) & 31u);
+            r.cnt += 1;
+            r.pos = p2;
+            if (a2 && p2 < e) {  // the second code also starts inside the segment
+                if (join(p2)) break;
+                r.cnt += 1;
+                r.pos = pos + ((e1 >> 24) & 31u);
+            }
+            run = r.pos < e;
+        } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
+            uint32_t sy, len;
+            bool eos;
+            lo_decode(w, lo, sy, len, eos);
+            if (len > rem) {
+                r.stop = kEnded;
+                run = false;
+            } else if (eos) {
+                r.stop = kEos;
+                run = false;
+            } else {
+                r.cnt += 1;
+                r.pos = pos + len;
+                run = r.pos < e;
+            }
+        } else {  // the next code does not fit: the literal ends here
+            r.stop = kEnded;
+            run = false;
+        }
+    }
+    return r;
+}
+
 // Whole-wave call (all 64 lanes, wave-uniform arguments): the literal's bits start at window bit
 // P0 (N bits), its output at image byte o0. Returns out_len and the hpk_status.
+//
+// A lane's start is only replaced by its left neighbour's stop when that walk came "through" its
+// segment; a lane whose left neighbour stopped (end of literal or EOS, possibly a spurious one on
+// a not-yet-synchronised walk) keeps its own start and walk. So a spurious stop does not silence
+// the lanes after it (a cascade of one lane per round); once corrected, the next lane re-walks
+// from the true start and, with the boundary mask, joins its old walk within a few codes. The
+// first lane that does not come through holds the literal's true end.
 __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, int kStore,
                                             uint32_t P0, uint32_t N, uint32_t o0, uint32_t& out_len, uint32_t& status) {
     const uint32_t j = threadIdx.x & 63u;
     const uint32_t S = max(32u, (N + 63u) >> 6);
-    const bool inrange = j * S < N;
-    const uint32_t e = (j + 1) * S;
-    uint32_t b = j * S, cnt = 0, stop = kEnded, pos = b;
-    bool dead = !inrange;
-    if (!dead) pos = seg_walk<false>(win32, lut, lo, out8, kStore, P0, N, b, e, 0, 0, cnt, stop);
-    // round r fixes lane r at the latest, so 64 rounds always suffice
+    const uint32_t s0 = j * S, e = (j + 1) * S;
+    uint32_t b = s0;
+    SegWalk wk = {b, 0u, (uint32_t)kEnded, 0ull};
+    auto walk = [&](bool resume) {
+        if (b >= N) {  // nothing left: a stop at the literal's end
+            wk = {b, 0u, (uint32_t)kEnded, 0ull};
+        } else if (S > 96u) {  // long segments: keep the boundary mask, re-walks join the old walk
+            wk = resume ? seg_record<true>(win32, lut, lo, P0, N, s0, b, e, wk)
+                        : seg_record<false>(win32, lut, lo, P0, N, s0, b, e, wk);
+        } else {  // short segments re-walk whole (cheaper than keeping the mask up)
+            wk.pos = seg_walk<false>(win32, lut, lo, out8, kStore, P0, N, b, e, 0, 0, wk.cnt, wk.stop);
+        }
+    };
+    walk(false);
+    // lane j's start only changes after lane j-1's stopped changing, so 64 rounds always suffice
     bool stuck = false;
     for (uint32_t round = 0;; ++round) {
         if (round > 64u) {
             stuck = true;
             break;
         }
-        const uint32_t lpos = __shfl_up(pos, 1);
-        const uint32_t lthrough = __shfl_up((uint32_t)(!dead && stop == kThrough), 1);
-        const uint32_t nb = j == 0 ? 0u : lpos;
-        const bool ndead = !inrange || (j != 0 && !lthrough);
-        const bool changed = ndead != dead || (!ndead && nb != b);
+        const uint32_t lpos = __shfl_up(wk.pos, 1);
+        const uint32_t lthrough = __shfl_up((uint32_t)(wk.stop == kThrough), 1);
+        const uint32_t nb = j == 0 ? 0u : (lthrough ? lpos : b);
+        const bool changed = nb != b;
         if (!__any(changed)) break;
         if (changed) {
             b = nb;
-            dead = ndead;
-            if (!dead) {
-                pos = seg_walk<false>(win32, lut, lo, out8, kStore, P0, N, b, e, 0, 0, cnt, stop);
-            } else {
-                pos = b;
-                cnt = 0;
-                stop = kEnded;
-            }
+            walk(true);
         }
     }
-    // output offsets: scan of the live lanes' counts
-    const uint32_t c = dead ? 0u : cnt;
+    // the literal ends in the first lane that does not come through (all through: the last lane)
+    const uint64_t nt = __ballot(wk.stop != kThrough);
+    const uint32_t L = nt ? (uint32_t)__builtin_ctzll(nt) : 63u;
+    const uint32_t c = j <= L ? wk.cnt : 0u;
     uint32_t incl = c;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -337,14 +424,11 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
         if (j >= (uint32_t)d) incl += y;
     }
     out_len = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    // the last live lane holds the literal's end (lane 0 always lives: N > 0)
-    const uint64_t live = __ballot(!dead);
-    const int sl = 63 - __builtin_clzll(live);
-    const uint32_t s_stop = (uint32_t)__builtin_amdgcn_readlane((int)stop, sl);
-    const uint32_t s_pos = (uint32_t)__builtin_amdgcn_readlane((int)pos, sl);
+    const uint32_t s_stop = (uint32_t)__builtin_amdgcn_readlane((int)wk.stop, (int)L);
+    const uint32_t s_pos = (uint32_t)__builtin_amdgcn_readlane((int)wk.pos, (int)L);
     status = s_stop == kEos ? (uint32_t)HPK_EOS_IN_STRING : residual_status(N - s_pos, win_at(win32, P0 + s_pos));
-    if (stuck || __any(stop == kStuck)) status = 0x7F;  // never expected: shows up as a bad status
-    if (!dead && c) {
+    if (stuck || __any(j <= L && wk.stop == kStuck)) status = 0x7F;  // never expected: a bad status
+    if (c) {
         uint32_t c2, st2;
         seg_walk<true>(win32, lut, lo, out8, kStore, P0, N, b, e, o0 + incl - c, o0 + N / 5u, c2, st2);
     }

@@ -102,6 +102,11 @@ def config3(codec, stream):
     d_len = torch.empty(w.n, dtype=torch.int32, device=dev)
     d_st = torch.empty(w.n, dtype=torch.uint8, device=dev)
     t_dec = cuda_time(lambda: codec.decode_into(enc_blob, enc_off32, d_out, doff, d_len, d_st, device=True), 5, stream)
+    # the same batch as the CPU encoder wrote it (a cross-check of the decode time)
+    c_blob = torch.from_numpy(w.enc_blob).to(dev)
+    c_off = torch.from_numpy(w.enc_off.astype(np.int64)).to(dev).to(torch.int32)
+    t_dec_cpu_enc = cuda_time(lambda: codec.decode_into(c_blob, c_off, d_out, doff, d_len, d_st, device=True), 5, stream)
+    codec.decode_into(enc_blob, enc_off32, d_out, doff, d_len, d_st, device=True)
     ok_st = not d_st.any().item()
     ok_len = bool(torch.equal(d_len.to(torch.int64), d_doff[1:] - d_doff[:-1]))
     dl = d_len.to(torch.int64)
@@ -118,6 +123,7 @@ def config3(codec, stream):
     emit({"config": "config3", "literals": w.n, "decoded_bytes": w.dec_bytes, "encoded_bytes": enc_bytes,
           "encode_us": round(t_enc * 1e6, 1), "encode_GiB_s_of_input": round(w.dec_bytes / t_enc / 2**30, 2),
           "decode_us": round(t_dec * 1e6, 1), "decode_GiB_s_of_input": round(enc_bytes / t_dec / 2**30, 2),
+          "decode_us_cpu_encoded_copy": round(t_dec_cpu_enc * 1e6, 1),
           "round_trip_bit_exact": ok_st and ok_len and ok_bytes, "encode_matches_oracle_sample": k})
 
 
