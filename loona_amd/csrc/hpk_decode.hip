@@ -44,7 +44,19 @@ constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2, kChu
 constexpr bool kAcc = false;
 constexpr int kCoop = 1;  // literals of >= 224 encoded bytes: one wave each (self-synchronising walk)
 using Geo = Geo12<kWaves, kW, kO, kQ>;
-#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched>
+#ifndef HPK_LONGDYN
+#define HPK_LONGDYN 1
+#endif
+#ifndef HPK_DEFER
+#define HPK_DEFER 0
+#endif
+constexpr int kLongDyn = HPK_LONGDYN;     // long literals: waves take the next one from an LDS counter
+constexpr int kDefer = HPK_DEFER;  // the previous fill's write-back issued during this decode
+#ifndef HPK_PREDST
+#define HPK_PREDST 1
+#endif
+constexpr int kPredSt = HPK_PREDST;  // unconditional byte stores in the lane step (dummy slots)
+#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt>
 
 static int g_debug_mode = -1;
 
@@ -56,7 +68,7 @@ int hpk_decode_setup() {
     return HPK_E_OK;  // the decode kernel's LDS is static: no attribute to set
 }
 
-// diagnostic stamps buffer (HPK_DEBUG_MODE=3): 4 x u64 per wave
+// diagnostic stamps buffer (HPK_DEBUG_MODE=3): 16 x u64 per wave
 static unsigned long long* g_dbg = nullptr;
 static size_t g_dbg_n = 0;
 
@@ -105,7 +117,7 @@ int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
             hipLaunchKernelGGL(DEC_KERNEL(2), grid, block, 0, c->stream, a);
             break;
         case 3: {
-            const size_t need = (size_t)blocks * kWaves * 4;
+            const size_t need = (size_t)blocks * kWaves * 16;
             if (need > g_dbg_n) {
                 (void)hipFree(g_dbg);
                 HIP_TRY(hipMalloc(&g_dbg, need * 8));

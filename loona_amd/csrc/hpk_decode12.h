@@ -37,6 +37,10 @@ struct Geo12 : Geo7<kWaves, kW, kO, kQ, true> {
     static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
 };
 
+#ifndef HPK_DEFER0
+#define HPK_DEFER0 2
+#endif
+
 // Longest-first buckets 0..14 hold the literals of >= 224 encoded bytes (lpt_bucket).
 constexpr uint32_t kLongBuckets = 15;
 
@@ -46,7 +50,7 @@ __device__ __forceinline__ void put8(uint8_t* __restrict__ out8, uint32_t pos, u
             out8[pos] = (uint8_t)v;
         else
             chk_report(1, pos, oend, 0);
-    } else if (kStore == kDword) {
+    } else if (kStore == kDword || kStore == kPred) {
         out8[pos] = (uint8_t)v;
     } else {
         asm volatile("" ::"v"(v));
@@ -59,7 +63,7 @@ __device__ __forceinline__ void put32(uint32_t* __restrict__ out32, uint32_t pos
             out32[pos] = v;
         else
             chk_report(2, pos, oend, 0);
-    } else if (kStore == kDword) {
+    } else if (kStore == kDword || kStore == kPred) {
         out32[pos] = v;
     } else {
         asm volatile("" ::"v"(v));
@@ -135,9 +139,12 @@ __device__ __forceinline__ void acc_push(Lit12& L, uint32_t* __restrict__ out32,
     L.cnt += g;
 }
 
+// kStore == kPred: the (up to) four byte stores of a step are unconditional, a byte that is not
+// output going to the lane's dummy slot out8[dmy] (no exec-mask branch around each store).
 template <int kStore, int kLook, bool kAcc>
 __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
-                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8) {
+                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8,
+                                           uint32_t dmy = 0) {
     uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
     const uint32_t d3 = win32[(L.X >> 5) + 2];  // the dword after d2, in case this step crosses one
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
@@ -149,7 +156,11 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     // a code longer than 12 bits (or EOS) starts here and may still fit
     bool park = (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);
     uint32_t pk = 0, g = 0;
-    if (!kAcc) {
+    if (!kAcc && kStore == kPred) {
+        out8[a1 ? L.o : dmy] = (uint8_t)e1;
+        out8[a2 ? L.o + 1 : dmy] = (uint8_t)(e1 >> 16);
+        L.o += (uint32_t)a1 + (uint32_t)a2;
+    } else if (!kAcc) {
         if (a1) put8(out8, L.o, e1, L.oend, kStore);
         if (a2) put8(out8, L.o + 1, e1 >> 16, L.oend, kStore);
         L.o += (uint32_t)a1 + (uint32_t)a2;
@@ -167,7 +178,11 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
         const uint32_t u2 = lut12(e2, rem2, b1, b2);
         b1 &= cont;
         b2 &= cont;
-        if (!kAcc) {
+        if (!kAcc && kStore == kPred) {
+            out8[b1 ? L.o : dmy] = (uint8_t)e2;
+            out8[b2 ? L.o + 1 : dmy] = (uint8_t)(e2 >> 16);
+            L.o += (uint32_t)b1 + (uint32_t)b2;
+        } else if (!kAcc) {
             if (b1) put8(out8, L.o, e2, L.oend, kStore);
             if (b2) put8(out8, L.o + 1, e2 >> 16, L.oend, kStore);
             L.o += (uint32_t)b1 + (uint32_t)b2;
@@ -437,21 +452,32 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // ------------------------------------------------------------------------------------------
 
 // kMode: 0 product; diagnostics (never the default): 1 no decode (fill structure only), 2 no
-// output stores, 3 product + per-wave stamps in a.dbg (cycles: total, in the decode loops,
-// steps, waiting at the fill-top barrier),
+// output stores, 3 product + 16 per-wave stamps in a.dbg (cycles: total, in the decode loops,
+// steps, waiting at the fill-top barrier, before the first fill, fill setup up to the entries,
+// fill setup from there to the decode, in long literals, the first fill's two setup parts, the
+// byte pass, the last write-back),
 // 4 checked stores (g_chk).
 // kCoop: 1 = long literals by whole waves (product), 0 = every literal by one lane (comparison).
 // kSched: 0 = lanes take queue slots dynamically (ballot + per-wave reservations), 1 = static
 // snake: lane i decodes slots i and 2*block-1-i of the longest-first queue, the second one's
 // entry and window dwords prefetched while the first decodes (no refill stall).
+// kLongDyn: 1 = a wave done with a long literal takes the next one from an LDS counter (the first
+// kWaves are dealt statically), 0 = static round-robin.
+// kDefer: 1 = the previous fill's write-back stores are issued from registers during this fill's
+// decode, one slot per iteration; 0 = all of them between the two decodes.
+// kPredSt: 1 = lane steps store every byte unconditionally (kPred), 0 = exec-masked stores.
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
-          int kCoop = 1, int kSched = 0>
+          int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
-    constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : kDword);
+    constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : (kPredSt ? kPred : kDword));
+    // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
+    constexpr int kImg = kStore == kPred ? kO - 256 : kO;
+    const uint32_t dmy = (uint32_t)kImg + (threadIdx.x & 63u) * 4u;
     static_assert(kChunk >= 64, "a refill can hand out 64 slots");
-    unsigned long long t_start = 0, t_dec = 0, n_steps = 0, n_fills = 0;
+    unsigned long long t_start = 0, t_dec = 0, n_steps = 0, n_fills = 0, t_pre = 0, t_setA = 0, t_setB = 0, t_long = 0,
+                       t_A0 = 0, t_B0 = 0, t_tail = 0, t_byte = 0;
     if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
     __shared__ __attribute__((aligned(16))) uint8_t smem[G::kLdsBytes];
     uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
@@ -512,6 +538,77 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
     };
+    // kDefer: the same write-back in two halves. flush_read takes the previous fill's image chunks,
+    // lengths and end bytes into registers before this fill decodes over the image; flush_slot(s)
+    // issues slot s of their stores (s < F: image round s, s == F: lengths, statuses, end bytes),
+    // one slot per decode iteration, so the stores drain while the fill decodes instead of
+    // stalling every wave at once between two decodes.
+    constexpr int F = G::kFlushRounds;
+    constexpr int kDefer0 = HPK_DEFER0;  // image rounds [0, kDefer0) are stored by flush_read itself
+    static_assert(F <= 16 && R <= 15, "flush slot bits");
+    uint4 f_c[F];
+    uint32_t f_lv[R];
+    uint32_t f_mask = 0, f_pv = 0, f_px = 0;  // bit r: chunk r; bit 16 + r: length r; bit 31: end byte
+    uint32_t f_c0 = 0, f_cur = 0;
+    int fs = F + 1;  // next slot to issue (F + 1: nothing pending); wave-uniform
+    auto flush_read = [&](uint32_t fcur, uint32_t fk, uint32_t G0, uint32_t G1) {
+        const uint32_t ob = G0 & ~15u;
+        const uint32_t c0 = ob >> 4, c1 = (G1 + 15) >> 4;
+        f_c0 = c0;
+        f_cur = fcur;
+        f_mask = 0;
+        if (kMode != 2) {
+            const uint4* l16 = reinterpret_cast<const uint4*>(s_out);
+#pragma unroll
+            for (int r = 0; r < F; ++r) {
+                const uint32_t ci = c0 + tid + (uint32_t)G::kBlock * r;
+                if (ci < c1 && (ci << 4) >= G0 && (ci << 4) + 16u <= G1) {
+                    if (r < kDefer0) {  // the first rounds go out now
+                        reinterpret_cast<uint4*>(a.out_base)[ci] = l16[ci - c0];
+                    } else {
+                        f_c[r] = l16[ci - c0];
+                        f_mask |= 1u << r;
+                    }
+                }
+            }
+            if (tid < 32) {
+                const uint32_t g = tid < 16 ? c0 << 4 : (c1 - 1) << 4;
+                const bool partial = !(g >= G0 && g + 16u <= G1) && (tid < 16 || c1 - 1 != c0);
+                const uint32_t x = g + (tid & 15u);
+                if (partial && x >= G0 && x < G1) {
+                    f_pv = s_out[x - ob];
+                    f_px = x;
+                    f_mask |= 1u << 31;
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = tid + (uint32_t)G::kBlock * r;
+            if (i < fk) {
+                f_lv[r] = s_lenst[i];
+                f_mask |= 1u << (16 + r);
+            }
+        }
+        fs = 0;
+    };
+    auto flush_slot = [&](int s) {
+        uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
+#pragma unroll
+        for (int r = 0; r < F; ++r)
+            if (s == r && ((f_mask >> r) & 1u)) g16[f_c0 + tid + (uint32_t)G::kBlock * r] = f_c[r];
+        if (s == F) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if ((f_mask >> (16 + r)) & 1u) {
+                    const uint32_t i = f_cur + tid + (uint32_t)G::kBlock * r;
+                    a.out_len[i] = f_lv[r] & 0xFFFFFFu;
+                    a.status[i] = (uint8_t)(f_lv[r] >> 24);
+                }
+            }
+            if (f_mask >> 31) a.out_base[f_px] = (uint8_t)f_pv;
+        }
+    };
     uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
 
     uint32_t cur = BA;
@@ -522,6 +619,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         gout = a.out_off[cur] + a.out_mis;
         prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
     }
+    if (kMode == 3) t_pre = __builtin_amdgcn_s_memtime() - t_start;
     while (cur < BB) {  // block-uniform
         const uint32_t cntl = min((uint32_t)kQ, BB - cur);
         const uint32_t base16 = gin & ~15u;
@@ -529,7 +627,11 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         unsigned long long tb0 = 0;
         if (kMode == 3) tb0 = __builtin_amdgcn_s_memtime();
         lds_barrier();  // previous fill decoded and its image read out: every LDS region is free
-        if (kMode == 3) n_fills += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: barrier wait)
+        if (kMode == 3) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            n_fills += t1 - tb0;  // (mode 3: barrier wait)
+            tb0 = t1;
+        }
         if (tid < 64) s_hist[tid] = 0;
         if (tid == 0) {
             s_ctr[0] = 0;
@@ -547,7 +649,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
             const uint32_t o0 = P.oo0[r] + a.out_mis, o1 = P.oo1[r] + a.out_mis;
             // fitting literals form a prefix (offsets are non-decreasing)
-            const bool fits = t < cntl && p1 - base16 <= (uint32_t)kW && o1 - ob16 <= (uint32_t)kO;
+            const bool fits = t < cntl && p1 - base16 <= (uint32_t)kW && o1 - ob16 <= (uint32_t)kImg;
             pos[r] = 0xFFFFFFFFu;
             if (fits) {
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
@@ -573,6 +675,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         if (lane == 0 && kw) atomicAdd(&s_ctr[0], kw);
         lds_barrier();
+        if (kMode == 3) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_setA += t1 - tb0;  // (mode 3: offsets in, entries made)
+            if (cur == BA) t_A0 = t1 - tb0;
+            tb0 = t1;
+        }
         const uint32_t k = s_ctr[0];
         if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global
             if (tid == 0) {
@@ -620,7 +728,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (pos[r] != 0xFFFFFFFFu) s_q[s_bbase[pos[r] >> 16] + (pos[r] & 0xFFFFu)] = make_uint2(ex[r], ey[r]);
-        const uint32_t nlong = kCoop ? s_bbase[kLongBuckets] : 0u;  // the queue's head: literals of >= 224 bytes
+        const uint32_t nlong = kCoop ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_bbase[kLongBuckets]) : 0u;  // the queue's head: literals of >= 224 bytes
         // the next fill's offsets and window: in flight during this fill's decode. Unconditional
         // (clamped past the range end), so no register phi forces a wait on the stores below.
         const uint32_t cur_next = cur + k;
@@ -629,150 +737,196 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             prefetch_fill<G::kBlock>(P, a, tid, c, min(c + (uint32_t)kQ, BB), gin_next & ~15u, rlast16);
         }
         // the previous fill's write-back: its image is read out before this fill decodes over it
-        if (pk) flush(pcur, pk, pG0, pG1);
+        if (pk) {
+            if (kDefer)
+                flush_read(pcur, pk, pG0, pG1);
+            else
+                flush(pcur, pk, pG0, pG1);
+        }
         pk = k;
         pcur = cur;
         pG0 = gout;
         pG1 = gout_next;
         lds_barrier();
         unsigned long long td0 = 0;
-        if (kMode == 3) td0 = __builtin_amdgcn_s_memtime();
+        if (kMode == 3) {
+            td0 = __builtin_amdgcn_s_memtime();
+            t_setB += td0 - tb0;  // (mode 3: window, queue, prefetch + write-back issued)
+            if (cur == BA) t_B0 = td0 - tb0;
+        }
         if (kMode == 1) {  // diagnostic: no decode; lengths from the queue keep the fill live
             for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
                 const uint2 e = s_q[tt];
                 s_lenst[e.y & 0xFFFu] = (e.x >> 16) + s_in[e.x & 0xFFFFu];
             }
         }
-        // long literals first (longest-first): one wave each, round-robin over the queue's head.
-        // Everything in this loop is wave-uniform and held in scalar registers: with a lane-0
-        // atomic or a branch on a vector value the compiler makes the loop divergent, and the
-        // cross-lane operations inside long_decode then run under a partial exec mask.
-        if (kMode != 1 && nlong) {
-            const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-            for (uint32_t jl = wv; jl < nlong; jl += kWaves) {
-                const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].x);
-                const uint32_t ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].y);
-                if (ey & kQ7Byte) continue;  // capacity below the bound: the byte pass below
-                uint32_t len, st;
-                long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
-                            (ey >> 12) & 0x1FFFFu, len, st);
-                if (lane == 0) s_lenst[ey & 0xFFFu] = len | (st << 24);
-            }
-        }
-        const uint32_t kl = k - nlong;  // lane-queue entries s_q[nlong, k)
-        if (kMode != 1 && kl && kSched == 0) {
-            const uint2* lq = s_q + nlong;
-            Lit12 L;
-            uint32_t t = tid;
-            uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
-            // Branch-free (re)start: lanes past the queue read a clamped entry and stay idle (no
-            // bits: rem = 0). The loop has no divergent exits, so the ballots see the whole wave.
-            auto begin = [&](uint32_t tt) {
-                const uint2 e = lq[min(tt, kl - 1)];
-                L.act = tt < kl && !(e.y & kQ7Byte);
-                L.idx = e.y & 0xFFFu;
-                const uint32_t nb = e.x >> 16;
-                const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
-                L.X = (e.x & 0xFFFFu) * 8u + 31u;
-                L.Eb = L.X + (L.act ? nb * 8u : 0u);
-                L.o = kAcc ? ob >> 2 : ob;
-                L.o0 = ob;
-                L.oend = kAcc ? (ob + nb * 8u / 5u + 3u) >> 2 : ob + nb * 8u / 5u;
-                L.cnt = 0;
-                L.acc = 0;
-                L.accn = 0;
-                L.st = HPK_OK;
-                L.prog = false;
-                lit12_load(L, win32);
-            };
-            begin(t);
-            for (;;) {
-#pragma unroll
-                for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out);
-                if (kMode == 3) n_steps += kRefillN;
-                const bool fin = t < kl && !L.prog;
-                if (__any(fin)) {
-                    if (fin && L.act) {
-                        if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
-                        s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+        // long literals first (longest-first): one wave each, the first kWaves dealt round-robin,
+        // then taken from an LDS counter as waves come free. Everything that steers this loop is
+        // wave-uniform and held in scalar registers (readlane of lane 0, never a branch on a vector
+        // value): a divergent loop would run long_decode's cross-lane operations under a partial
+        // exec mask.
+        // (the long-literal phase and the lane phase are lambdas so that with kDefer the phase
+        // holding the write-back registers is a separate code path: long_decode never runs with
+        // them live, and the decode keeps its registers)
+        auto long_phase = [&]() {
+            if (kMode != 1 && nlong) {
+                const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+                for (uint32_t jl = wv; jl < nlong;) {
+                    const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].x);
+                    const uint32_t ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].y);
+                    if (!(ey & kQ7Byte)) {  // (capacity below the bound: the byte pass below)
+                        uint32_t len, st;
+                        long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
+                                    (ey >> 12) & 0x1FFFFu, len, st);
+                        if (lane == 0) s_lenst[ey & 0xFFFu] = len | (st << 24);
                     }
-                    const bool free_lane = fin || t >= kl;
-                    const uint64_t fm = __ballot(free_lane);
-                    const uint32_t rank =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-                    // free lanes take the wave's reserved slots [qb, qe) in rank order; when those
-                    // run short the wave reserves kChunk more with one LDS atomic
-                    const uint32_t need = (uint32_t)__popcll(fm), have = qe - qb;
-                    uint32_t base = qb + rank;
-                    if (have < need) {  // wave-uniform
-                        uint32_t nb = 0;
-                        if (rank == 0 && free_lane) nb = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
-                        nb = (uint32_t)__builtin_amdgcn_readlane((int)nb, (int)__builtin_ctzll(fm));
-                        if (rank >= have) base = nb + (rank - have);
-                        qb = nb + (need - have);
-                        qe = nb + kChunk;
+                    if (kLongDyn) {  // the next long literal: one LDS atomic per wave, read from lane 0
+                        uint32_t nx = 0;
+                        if (lane == 0) nx = atomicAdd(&s_ctr[4], 1u) + (uint32_t)kWaves;
+                        jl = (uint32_t)__builtin_amdgcn_readlane((int)nx, 0);
                     } else {
-                        qb += need;
-                    }
-                    qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
-                    qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
-                    if (free_lane) {
-                        t = base;
-                        begin(base);
+                        jl += kWaves;
                     }
                 }
-                if (!__any(t < kl)) break;
             }
-        }
-        if (kMode != 1 && kl && kSched == 1) {
-            static_assert(kSched != 1 || kQ <= 2 * G::kBlock, "static snake: two literals per lane at most");
-            const uint2* lq = s_q + nlong;
-            Lit12 L, N;  // the literal being decoded and the lane's next one (prefetched)
-            auto load = [&](Lit12& T, uint32_t tt) {
-                const uint2 e = lq[min(tt, kl - 1)];
-                T.act = tt < kl && !(e.y & kQ7Byte);
-                T.idx = e.y & 0xFFFu;
-                const uint32_t nb = e.x >> 16;
-                const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
-                T.X = (e.x & 0xFFFFu) * 8u + 31u;
-                T.Eb = T.X + (T.act ? nb * 8u : 0u);
-                T.o = kAcc ? ob >> 2 : ob;
-                T.o0 = ob;
-                T.oend = kAcc ? (ob + nb * 8u / 5u + 3u) >> 2 : ob + nb * 8u / 5u;
-                T.cnt = 0;
-                T.acc = 0;
-                T.accn = 0;
-                T.st = HPK_OK;
-                T.prog = false;
-                lit12_load(T, win32);
-            };
-            load(L, tid);
-            const uint32_t t2 = 2u * G::kBlock - 1u - tid;
-            bool nv = t2 < kl;  // a second literal is waiting in N
-            load(N, t2);
-            for (;;) {
-#pragma unroll
-                for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out);
-                if (kMode == 3) n_steps += kRefillN;
-                const bool fin = !L.prog;  // no progress in the last step: finished (or idle)
-                if (__any(fin)) {
-                    if (fin && L.act) {
-                        if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
-                        s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
-                    }
-                    if (fin) {
-                        if (nv) {
-                            L = N;
-                            nv = false;
+            if (kMode == 3) t_long += __builtin_amdgcn_s_memtime() - td0;
+        };
+        const uint32_t kl = k - nlong;  // lane-queue entries s_q[nlong, k)
+        auto lane_phase = [&](auto dtag) {
+            constexpr bool D = decltype(dtag)::value;  // issue write-back slots from the loop
+            if (kMode != 1 && kl && kSched == 0) {
+                const uint2* lq = s_q + nlong;
+                Lit12 L;
+                uint32_t t = tid;
+                uint32_t qb = 0, qe = 0;  // queue slots reserved by this wave, not yet handed out
+                // Branch-free (re)start: lanes past the queue read a clamped entry and stay idle (no
+                // bits: rem = 0). The loop has no divergent exits, so the ballots see the whole wave.
+                auto begin = [&](uint32_t tt) {
+                    const uint2 e = lq[min(tt, kl - 1)];
+                    L.act = tt < kl && !(e.y & kQ7Byte);
+                    L.idx = e.y & 0xFFFu;
+                    const uint32_t nb = e.x >> 16;
+                    const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
+                    L.X = (e.x & 0xFFFFu) * 8u + 31u;
+                    L.Eb = L.X + (L.act ? nb * 8u : 0u);
+                    L.o = kAcc ? ob >> 2 : ob;
+                    L.o0 = ob;
+                    L.oend = kAcc ? (ob + nb * 8u / 5u + 3u) >> 2 : ob + nb * 8u / 5u;
+                    L.cnt = 0;
+                    L.acc = 0;
+                    L.accn = 0;
+                    L.st = HPK_OK;
+                    L.prog = false;
+                    lit12_load(L, win32);
+                };
+                begin(t);
+                for (;;) {
+    #pragma unroll
+                    for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
+                    if (kMode == 3) n_steps += kRefillN;
+                    const bool fin = t < kl && !L.prog;
+                    if (__any(fin)) {
+                        if (fin && L.act) {
+                            if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
+                            s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+                        }
+                        const bool free_lane = fin || t >= kl;
+                        const uint64_t fm = __ballot(free_lane);
+                        const uint32_t rank =
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+                        // free lanes take the wave's reserved slots [qb, qe) in rank order; when those
+                        // run short the wave reserves kChunk more with one LDS atomic
+                        const uint32_t need = (uint32_t)__popcll(fm), have = qe - qb;
+                        uint32_t base = qb + rank;
+                        if (have < need) {  // wave-uniform
+                            uint32_t nb = 0;
+                            if (rank == 0 && free_lane) nb = atomicAdd(&s_ctr[1], (uint32_t)kChunk);
+                            nb = (uint32_t)__builtin_amdgcn_readlane((int)nb, (int)__builtin_ctzll(fm));
+                            if (rank >= have) base = nb + (rank - have);
+                            qb = nb + (need - have);
+                            qe = nb + kChunk;
                         } else {
-                            L.act = false;
+                            qb += need;
+                        }
+                        qb = (uint32_t)__builtin_amdgcn_readfirstlane((int)qb);
+                        qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)qe);
+                        if (free_lane) {
+                            t = base;
+                            begin(base);
                         }
                     }
+                    if (!__any(t < kl)) break;
                 }
-                if (!__any(L.act || nv)) break;
             }
+            if (kMode != 1 && kl && kSched == 1) {
+                static_assert(kSched != 1 || kQ <= 2 * G::kBlock, "static snake: two literals per lane at most");
+                const uint2* lq = s_q + nlong;
+                Lit12 L, N;  // the literal being decoded and the lane's next one (prefetched)
+                auto load = [&](Lit12& T, uint32_t tt) {
+                    const uint2 e = lq[min(tt, kl - 1)];
+                    T.act = tt < kl && !(e.y & kQ7Byte);
+                    T.idx = e.y & 0xFFFu;
+                    const uint32_t nb = e.x >> 16;
+                    const uint32_t ob = (e.y >> 12) & 0x1FFFFu;
+                    T.X = (e.x & 0xFFFFu) * 8u + 31u;
+                    T.Eb = T.X + (T.act ? nb * 8u : 0u);
+                    T.o = kAcc ? ob >> 2 : ob;
+                    T.o0 = ob;
+                    T.oend = kAcc ? (ob + nb * 8u / 5u + 3u) >> 2 : ob + nb * 8u / 5u;
+                    T.cnt = 0;
+                    T.acc = 0;
+                    T.accn = 0;
+                    T.st = HPK_OK;
+                    T.prog = false;
+                    lit12_load(T, win32);
+                };
+                load(L, tid);
+                const uint32_t t2 = 2u * G::kBlock - 1u - tid;
+                bool nv = t2 < kl;  // a second literal is waiting in N
+                load(N, t2);
+                for (;;) {
+    #pragma unroll
+                    for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
+                    if (kMode == 3) n_steps += kRefillN;
+                    if (D && fs <= F) flush_slot(fs++);
+                    const bool fin = !L.prog;  // no progress in the last step: finished (or idle)
+                    if (__any(fin)) {
+                        if (fin && L.act) {
+                            if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
+                            s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+                        }
+                        if (fin) {
+                            if (nv) {
+                                L = N;
+                                nv = false;
+                            } else {
+                                L.act = false;
+                            }
+                        }
+                    }
+                    if (!__any(L.act || nv)) break;
+                }
+            }
+        };
+        if (kDefer) {
+            if (nlong) {  // write-back first, then the long literals
+                while (fs <= F) flush_slot(fs++);
+                long_phase();
+                lane_phase(std::false_type{});
+            } else {
+                lane_phase(std::true_type{});
+            }
+        } else {
+            long_phase();
+            lane_phase(std::false_type{});
         }
-        if (kMode == 3) t_dec += __builtin_amdgcn_s_memtime() - td0;
+        if (kDefer)
+            while (fs <= F) flush_slot(fs++);  // what the decode loops did not issue
+        unsigned long long tq0 = 0;
+        if (kMode == 3) {
+            tq0 = __builtin_amdgcn_s_memtime();
+            t_dec += tq0 - td0;
+        }
         // literals whose output region is below the decoded bound (or not dword-aligned for the
         // dword stores): byte stores into the image with a capacity check per byte
         for (uint32_t tt = tid; kMode != 1 && tt < k; tt += G::kBlock) {
@@ -786,20 +940,31 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 s_lenst[i] = B.cnt | (lit_status(B) << 24);
             }
         }
+        if (kMode == 3) t_byte += __builtin_amdgcn_s_memtime() - tq0;
         cur = cur_next;
         gin = gin_next;
         gout = gout_next;
     }
+    if (kMode == 3) t_tail = __builtin_amdgcn_s_memtime();
     if (pk) {
         lds_barrier();
         flush(pcur, pk, pG0, pG1);
     }
     if (kMode == 3 && lane == 0) {
         const uint64_t gwi = (uint64_t)blockIdx.x * kWaves + (tid >> 6);
-        a.dbg[gwi * 4 + 0] = __builtin_amdgcn_s_memtime() - t_start;
-        a.dbg[gwi * 4 + 1] = t_dec;
-        a.dbg[gwi * 4 + 2] = n_steps;
-        a.dbg[gwi * 4 + 3] = n_fills;
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        a.dbg[gwi * 16 + 0] = t_end - t_start;
+        a.dbg[gwi * 16 + 1] = t_dec;
+        a.dbg[gwi * 16 + 2] = n_steps;
+        a.dbg[gwi * 16 + 3] = n_fills;
+        a.dbg[gwi * 16 + 4] = t_pre;
+        a.dbg[gwi * 16 + 5] = t_setA;
+        a.dbg[gwi * 16 + 6] = t_setB;
+        a.dbg[gwi * 16 + 7] = t_long;
+        a.dbg[gwi * 16 + 8] = t_A0;
+        a.dbg[gwi * 16 + 9] = t_B0;
+        a.dbg[gwi * 16 + 10] = t_byte;
+        a.dbg[gwi * 16 + 11] = t_end - t_tail;
     }
 }
 

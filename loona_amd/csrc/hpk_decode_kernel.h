@@ -49,7 +49,8 @@ struct Lit {
     bool park;      // step 7: waiting at the next refill point for a leading-ones lookup
 };
 
-enum StoreMode { kDword = 0, kNoStore = 1, kChecked = 3 };
+enum StoreMode { kDword = 0, kNoStore = 1, kChecked = 3, kPred = 4 };  // kPred: kDword, lane steps store
+// unconditionally, a byte that is not output going to a per-lane dummy slot
 
 // Bitstream sources: a staged LDS window, or global memory (clamped to the batch).
 struct LdsSrc {

@@ -1,8 +1,20 @@
 // hpk_encode.hip — gfx950 batched canonical Huffman encode (RFC 7541 §5.2; the H-bit branch
 // crates/loona-hpack/src/encoder.rs:299-307 never takes — the reference has no encoder).
 //
-// v1: one lane per literal; the 257-entry code table sits in LDS; codes are packed MSB-first into
-// a 64-bit accumulator, flushed a byte at a time, and the tail is padded with EOS MSBs (ones).
+// v2 (hpk_encode2): one 1024-thread workgroup per CU owns a contiguous literal range and encodes it
+// in tiles of whole literals (<= 32 KiB of input, <= 2048 literals, output span <= the LDS image):
+//   * every thread owns 32 consecutive input bytes of the tile (two 16-byte loads, in registers);
+//   * a segmented scan of per-byte code lengths over the 1024 threads (literal starts reset it)
+//     gives each byte its bit offset inside its literal;
+//   * each byte's code is OR-ed into an LDS image of the tile's output span (big-endian dwords,
+//     ds_or_b32, one or two per code), clipped at the literal's capacity;
+//   * one thread per literal then pads the last byte with EOS's most significant bits (ones) and
+//     writes out_len / status; the image goes out with 16-byte stores (bytewise in the span's two
+//     end chunks, which neighbouring tiles own).
+// A literal too large for a tile is encoded by one lane straight to global memory (v1's loop).
+// v1 (hpk_encode_kernel, one lane per literal) stays as the comparison build (HPK_ENCODE_V1=1).
+#include <stdlib.h>
+
 #include "hpk_device.h"
 
 namespace {
@@ -16,7 +28,46 @@ struct EncodeArgs {
     uint32_t* out_len;
     uint8_t* status;
     const uint32_t* codes;  // [0,257): right-aligned code, [257,514): length
+    // v2: 16-byte aligned bases and the blobs' misalignment (offsets are blob-relative)
+    const uint8_t* in_base;
+    uint32_t in_mis;
+    uint8_t* out_base;
+    uint32_t out_mis;
 };
+
+// One literal, one lane, global memory: v1's loop (also the large-literal path of v2).
+__device__ __forceinline__ void encode_serial(const EncodeArgs& a, const uint32_t* code, const uint8_t* len,
+                                              uint32_t i) {
+    const uint32_t s = a.in_off[i], e = a.in_off[i + 1];
+    const uint32_t o0 = a.out_off[i], ocap = a.out_off[i + 1] - o0;
+    uint8_t* out = a.out_blob + o0;
+    uint64_t acc = 0;
+    int nb = 0;
+    uint32_t o = 0;
+    uint32_t st = HPK_OK;
+    for (uint32_t p = s; p < e; ++p) {
+        const uint32_t b = a.in_blob[p];
+        acc = (acc << len[b]) | code[b];
+        nb += len[b];
+        while (nb >= 8) {
+            nb -= 8;
+            if (o >= ocap) {
+                st = HPK_OUTPUT_OVERFLOW;
+                break;
+            }
+            out[o++] = (uint8_t)(acc >> nb);
+        }
+        if (st) break;
+    }
+    if (!st && nb) {
+        if (o >= ocap)
+            st = HPK_OUTPUT_OVERFLOW;
+        else
+            out[o++] = (uint8_t)((acc << (8 - nb)) | (0xFFu >> nb));
+    }
+    a.out_len[i] = o;
+    a.status[i] = (uint8_t)st;
+}
 
 #define ENC_BLOCK 256
 
@@ -28,45 +79,264 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
         s_len[threadIdx.x] = (uint8_t)a.codes[257 + threadIdx.x];
     }
     __syncthreads();
-    for (uint32_t i = blockIdx.x * ENC_BLOCK + threadIdx.x; i < a.n; i += gridDim.x * ENC_BLOCK) {
-        const uint32_t s = a.in_off[i], e = a.in_off[i + 1];
-        const uint32_t o0 = a.out_off[i], ocap = a.out_off[i + 1] - o0;
-        uint8_t* out = a.out_blob + o0;
-        uint64_t acc = 0;
-        int nb = 0;
-        uint32_t o = 0;
-        uint32_t st = HPK_OK;
-        for (uint32_t p = s; p < e; ++p) {
-            const uint32_t b = a.in_blob[p];
-            acc = (acc << s_len[b]) | s_code[b];
-            nb += s_len[b];
-            while (nb >= 8) {
-                nb -= 8;
-                if (o >= ocap) { st = HPK_OUTPUT_OVERFLOW; break; }
-                out[o++] = (uint8_t)(acc >> nb);
-            }
-            if (st) break;
-        }
-        if (!st && nb) {
-            if (o >= ocap) st = HPK_OUTPUT_OVERFLOW;
-            else out[o++] = (uint8_t)((acc << (8 - nb)) | (0xFFu >> nb));
-        }
-        a.out_len[i] = o;
-        a.status[i] = (uint8_t)st;
+    for (uint32_t i = blockIdx.x * ENC_BLOCK + threadIdx.x; i < a.n; i += gridDim.x * ENC_BLOCK)
+        encode_serial(a, s_code, s_len, i);
+}
+
+// ---------------------------------------------------------------------------------------------
+// v2
+
+constexpr int kEB = 1024;                 // threads per workgroup (16 waves)
+constexpr int kEBytes = 32;               // input bytes per thread per tile
+constexpr int kETile = kEB * kEBytes;     // 32 KiB of input per tile
+constexpr int kEO = 112 * 1024;           // LDS output image (bytes)
+constexpr int kEQ = 2048;                 // literals per tile
+constexpr int kEMeta = kEQ / kEB;         // offset rounds per thread
+
+struct EncLds {
+    uint32_t img[kEO / 4];       // the tile's output span, big-endian dwords
+    uint32_t ioff[kEQ + 1];      // input offsets of the tile's literals, relative to the tile base
+    uint32_t ooff[kEQ + 1];      // output offsets, relative to the image base
+    uint32_t bits[kEQ];          // encoded bits per literal (set by the thread holding its last byte)
+    uint2 tab[256];              // (code, length)
+    uint32_t code1[256];         // serial path: codes
+    uint8_t len1[256];           // serial path: lengths
+    uint32_t wf[16], wv[16];     // per-wave scan totals
+    uint32_t ctr[4];             // [0] literals in the tile
+};
+static_assert(sizeof(EncLds) <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+
+__device__ __forceinline__ void lds_barrier_e() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// OR a code of `len` bits (right-aligned in c) into the big-endian image at bit q.
+__device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, uint32_t len) {
+    const uint32_t d = q >> 5, r = q & 31u;
+    if (r + len <= 32u) {
+        atomicOr(&img[d], c << (32u - r - len));
+    } else {
+        atomicOr(&img[d], c >> (r + len - 32u));
+        atomicOr(&img[d + 1], c << (64u - r - len));
     }
 }
 
+__global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
+    __shared__ __attribute__((aligned(16))) EncLds S;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    if (tid < 256) {
+        const uint32_t c = a.codes[tid], l = a.codes[257 + tid];
+        S.tab[tid] = make_uint2(c, l);
+        S.code1[tid] = c;
+        S.len1[tid] = (uint8_t)l;
+    }
+    const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
+    const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+    const uint32_t in_end = a.in_off[a.n] + a.in_mis;
+    const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
+    const uint4* g_in = reinterpret_cast<const uint4*>(a.in_base);
+    uint32_t cur = BA;
+    while (cur < BB) {  // block-uniform
+        const uint32_t cntl = min((uint32_t)kEQ, BB - cur);
+        const uint32_t gin = a.in_off[cur] + a.in_mis, gout = a.out_off[cur] + a.out_mis;
+        const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
+        // the tile's input chunks: in flight while the offsets are sorted out
+        uint4 ch[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) ch[r] = g_in[min((base16 >> 4) + 2u * tid + (uint32_t)r, last16)];
+        lds_barrier_e();  // the previous tile's image is out
+        if (tid == 0) S.ctr[0] = 0;
+        {  // clear the image
+            uint4* i16 = reinterpret_cast<uint4*>(S.img);
+            for (uint32_t c = tid; c < (uint32_t)kEO / 16; c += kEB) i16[c] = make_uint4(0, 0, 0, 0);
+        }
+        lds_barrier_e();
+        // which literals fit (a prefix: offsets are non-decreasing)
+        uint32_t kw = 0;
+#pragma unroll
+        for (int r = 0; r < kEMeta; ++r) {
+            const uint32_t t = tid + (uint32_t)kEB * r;
+            bool fits = false;
+            uint32_t i0 = 0, i1 = 0, o0 = 0, o1 = 0;
+            if (t < cntl) {
+                i0 = a.in_off[cur + t] + a.in_mis;
+                i1 = a.in_off[cur + t + 1] + a.in_mis;
+                o0 = a.out_off[cur + t] + a.out_mis;
+                o1 = a.out_off[cur + t + 1] + a.out_mis;
+                fits = i1 - base16 <= (uint32_t)kETile && o1 - ob16 <= (uint32_t)kEO;
+            }
+            if (fits) {
+                S.ioff[t] = i0 - base16;
+                S.ooff[t] = o0 - ob16;
+                S.ioff[t + 1] = i1 - base16;  // (the same value literal t + 1 writes)
+                S.ooff[t + 1] = o1 - ob16;
+                S.bits[t] = 0;
+            }
+            kw += (uint32_t)__popcll(__ballot(fits));
+        }
+        if (lane == 0 && kw) atomicAdd(&S.ctr[0], kw);
+        lds_barrier_e();
+        const uint32_t k = S.ctr[0];
+        if (k == 0) {  // literal `cur` alone exceeds a tile: one lane, global memory
+            if (tid == 0) encode_serial(a, S.code1, S.len1, cur);
+            cur += 1;
+            continue;
+        }
+        const uint32_t xb = S.ioff[0], xe = S.ioff[k];  // the tile's input bytes [xb, xe)
+        // this thread's bytes [x0, x1) and the literal holding x0
+        const uint32_t x0 = max(tid * (uint32_t)kEBytes, xb), x1 = min(tid * (uint32_t)kEBytes + kEBytes, xe);
+        const bool any = x0 < x1;
+        uint32_t li = 0;
+        if (any) {  // largest li < k with ioff[li] <= x0 (a non-empty literal)
+            uint32_t lo = 0, hi = k - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (S.ioff[mid] <= x0)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            li = lo;
+        }
+        const bool f0 = any && S.ioff[li] == x0;  // the thread's first byte starts a literal
+        auto byte_at = [&](uint32_t j) -> uint32_t {  // input byte 32 * tid + j
+            const uint4 c = ch[j >> 4];
+            const uint32_t w = (j & 8u) ? ((j & 4u) ? c.w : c.z) : ((j & 4u) ? c.y : c.x);
+            return (w >> (8u * (j & 3u))) & 0xFFu;
+        };
+        // pass 1: (a literal starts in the thread's bytes, bits since the last start)
+        uint32_t f = f0 ? 1u : 0u, v = 0;
+        if (any) {
+            uint32_t lj = li, nj = S.ioff[li + 1];
+            for (uint32_t x = x0; x < x1; ++x) {
+                while (x >= nj) {  // a literal starts at x (empty ones skipped)
+                    ++lj;
+                    nj = S.ioff[lj + 1];
+                    f = 1u;
+                    v = 0;
+                }
+                v += S.tab[byte_at(x - tid * (uint32_t)kEBytes)].y;
+            }
+        }
+        // segmented exclusive scan over the workgroup: the carry into each thread's first literal
+        uint32_t fi = f, vi = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t pf = __shfl_up(fi, d), pv = __shfl_up(vi, d);
+            if (lane >= (uint32_t)d) {
+                vi = fi ? vi : vi + pv;
+                fi |= pf;
+            }
+        }
+        if (lane == 63) {
+            S.wf[wv] = fi;
+            S.wv[wv] = vi;
+        }
+        lds_barrier_e();
+        uint32_t cw = 0;  // carry into this wave's lane 0
+        for (uint32_t j = 0; j < wv; ++j) cw = S.wf[j] ? S.wv[j] : cw + S.wv[j];
+        uint32_t ef = __shfl_up(fi, 1), ev = __shfl_up(vi, 1);
+        if (lane == 0) {
+            ef = 0;
+            ev = 0;
+        }
+        const uint32_t carry = ef ? ev : cw + ev;
+        // pass 2: codes into the image, clipped at each literal's capacity
+        if (any) {
+            uint32_t lj = li, nj = S.ioff[li + 1];
+            uint32_t bp = f0 ? 0u : carry;
+            uint32_t ob = S.ooff[li] * 8u, cap = S.ooff[li + 1] * 8u - ob;
+            for (uint32_t x = x0; x < x1; ++x) {
+                while (x >= nj) {
+                    ++lj;
+                    nj = S.ioff[lj + 1];
+                    bp = 0;
+                    ob = S.ooff[lj] * 8u;
+                    cap = S.ooff[lj + 1] * 8u - ob;
+                }
+                const uint2 e = S.tab[byte_at(x - tid * (uint32_t)kEBytes)];
+                if (bp + e.y <= cap) {
+                    img_or(S.img, ob + bp, e.x, e.y);
+                } else if (bp < cap) {  // overflow: the bits that still fit
+                    const uint32_t keep = cap - bp;
+                    img_or(S.img, ob + bp, e.x >> (e.y - keep), keep);
+                }
+                bp += e.y;
+                if (x + 1 == nj) S.bits[lj] = bp;  // the literal's last byte
+            }
+        }
+        lds_barrier_e();
+        // per literal: EOS padding, out_len, status
+#pragma unroll
+        for (int r = 0; r < kEMeta; ++r) {
+            const uint32_t t = tid + (uint32_t)kEB * r;
+            if (t < k) {
+                const uint32_t bits = S.bits[t];
+                const uint32_t cap = S.ooff[t + 1] - S.ooff[t];
+                const uint32_t nbytes = (bits + 7u) >> 3;
+                const bool over = nbytes > cap;
+                if (!over && (bits & 7u)) {
+                    const uint32_t pad = 8u - (bits & 7u);
+                    img_or(S.img, S.ooff[t] * 8u + bits, (1u << pad) - 1u, pad);
+                }
+                a.out_len[cur + t] = over ? cap : nbytes;
+                a.status[cur + t] = (uint8_t)(over ? HPK_OUTPUT_OVERFLOW : HPK_OK);
+            }
+        }
+        lds_barrier_e();
+        {  // write the image back: bytes [G0, G1) of the image (relative to ob16)
+            const uint32_t G0 = S.ooff[0], G1 = S.ooff[k];
+            const uint32_t c1 = (G1 + 15u) >> 4;
+            const uint4* i16 = reinterpret_cast<const uint4*>(S.img);
+            uint4* g16 = reinterpret_cast<uint4*>(a.out_base + ob16);
+            for (uint32_t c = tid; c < c1; c += kEB) {
+                if ((c << 4) >= G0 && (c << 4) + 16u <= G1) {
+                    const uint4 w = i16[c];
+                    g16[c] = make_uint4(__builtin_bswap32(w.x), __builtin_bswap32(w.y), __builtin_bswap32(w.z),
+                                        __builtin_bswap32(w.w));
+                }
+            }
+            if (tid < 32) {  // the partial chunks at the two ends, one byte per lane
+                const uint32_t g = tid < 16 ? 0u : (c1 - 1u) << 4;
+                const bool partial = !(g >= G0 && g + 16u <= G1) && (tid < 16 || c1 - 1u != 0u);
+                const uint32_t x = g + (tid & 15u);
+                if (partial && x >= G0 && x < G1) {
+                    const uint32_t w = S.img[x >> 2];
+                    a.out_base[ob16 + x] = (uint8_t)(w >> (24u - 8u * (x & 3u)));
+                }
+            }
+        }
+        cur += k;
+    }
+}
+
+static int g_encode_v1 = -1;
 
 }  // namespace
 
 int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
                       const uint32_t* out_off, uint32_t* out_len, uint8_t* status) {
+    if (g_encode_v1 < 0) {
+        const char* e = getenv("HPK_ENCODE_V1");
+        g_encode_v1 = e && atoi(e) ? 1 : 0;
+    }
     EncodeArgs a{in_blob, in_off, n, out_blob, out_off, out_len, status, c->d_codes};
-    uint64_t blocks = ((uint64_t)n + ENC_BLOCK - 1) / ENC_BLOCK;
-    const uint64_t max_blocks = (uint64_t)c->num_cu * 8;
-    if (blocks > max_blocks) blocks = max_blocks;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(hpk_encode_kernel, dim3((uint32_t)blocks), dim3(ENC_BLOCK), 0, c->stream, a);
+    const uintptr_t ip = (uintptr_t)in_blob, op = (uintptr_t)out_blob;
+    a.in_base = (const uint8_t*)(ip & ~(uintptr_t)15);
+    a.in_mis = (uint32_t)(ip & 15);
+    a.out_base = (uint8_t*)(op & ~(uintptr_t)15);
+    a.out_mis = (uint32_t)(op & 15);
+    if (g_encode_v1) {
+        uint64_t blocks = ((uint64_t)n + ENC_BLOCK - 1) / ENC_BLOCK;
+        const uint64_t max_blocks = (uint64_t)c->num_cu * 8;
+        if (blocks > max_blocks) blocks = max_blocks;
+        if (blocks < 1) blocks = 1;
+        hipLaunchKernelGGL(hpk_encode_kernel, dim3((uint32_t)blocks), dim3(ENC_BLOCK), 0, c->stream, a);
+    } else {
+        // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
+        uint64_t blocks = ((uint64_t)n + 63) / 64;
+        if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
+        if (blocks < 1) blocks = 1;
+        hipLaunchKernelGGL(hpk_encode2, dim3((uint32_t)blocks), dim3(kEB), 0, c->stream, a);
+    }
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
 }

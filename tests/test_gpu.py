@@ -184,6 +184,72 @@ def test_encode_matches_oracle(codec):
     compare_batches(gpu_encode(codec, blob, off), oracle_encode_batch(blob, off), "encode")
 
 
+@pytest.mark.parametrize("shift", [1, 3, 13])
+def test_encode_unaligned_bases(codec, shift):
+    """Encode v2 reads 16-byte chunks from a rounded-down base and writes a tile's output span with
+    16-byte stores: unaligned input and output bases, empty literals among them."""
+    from hpk_util import oracle_encode
+
+    rng = np.random.default_rng(11 + shift)
+    lens = rng.integers(0, 90, size=3000)
+    lens[::7] = 0
+    strs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+    blob, off = pack(strs)
+    pad = np.zeros(blob.size + shift + 1, np.uint8)
+    pad[shift : shift + blob.size] = blob
+    dblob = to_dev(pad)[shift:]
+    doff = to_dev(np.asarray(off, np.int64).astype(np.int32))
+    from loona_amd.batch import encode_offsets_torch
+
+    oo = encode_offsets_torch(doff)
+    big = torch.full((int(oo[-1].item()) + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    out = big[shift:]
+    n = len(strs)
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    codec.encode_into(dblob, doff, out, oo, ol, st, device=True, sync=True)
+    o, oon, oln, stn = out.cpu().numpy(), oo.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy()
+    assert not stn.any()
+    for i in range(n):
+        want = oracle_encode(strs[i])
+        assert int(oln[i]) == len(want), i
+        assert o[oon[i] : oon[i] + oln[i]].tobytes() == want, i
+    assert (big[:shift].cpu().numpy() == 0x5A).all()  # nothing before the output base
+
+
+def test_encode_small_capacity_and_huge_literal(codec):
+    """Capacities below the encoded size: status HPK_OUTPUT_OVERFLOW, out_len = capacity, the bytes
+    are the encoding's prefix and nothing is written past a region. A 70 KB literal (larger than a
+    tile) takes the one-lane path."""
+    from hpk_util import oracle_encode
+
+    rng = np.random.default_rng(5)
+    strs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 60, size=500)]
+    strs.append(bytes(rng.integers(0, 256, 70000, dtype=np.uint8)))
+    strs.append(b"www.example.com")
+    blob, off = pack(strs)
+    n = len(strs)
+    want = [oracle_encode(s) for s in strs]
+    cap = np.array([max(1, len(w) - (i % 3)) for i, w in enumerate(want)], np.int64)  # some short by 1 or 2
+    oo = np.zeros(n + 1, np.int64)
+    np.cumsum(cap, out=oo[1:])
+    dblob, doff = to_dev(blob), to_dev(off.astype(np.int32))
+    doo = to_dev(oo.astype(np.int32))
+    out = torch.full((int(oo[-1]) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    codec.encode_into(dblob, doff, out, doo, ol, st, device=True, sync=True)
+    o, oln, stn = out.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy()
+    for i in range(n):
+        c = int(cap[i])
+        if len(want[i]) <= c:
+            assert stn[i] == 0 and int(oln[i]) == len(want[i]), i
+        else:
+            assert stn[i] == 4 and int(oln[i]) == c, i
+        assert o[oo[i] : oo[i] + oln[i]].tobytes() == want[i][: int(oln[i])], i
+    assert (o[int(oo[-1]) :] == 0xAB).all()
+
+
 def test_config2_full_roundtrip(codec):
     """BASELINE config 2 at full size (1M literals): GPU decode of the canonical encoding gives back
     the generated strings exactly (size-independent property); a 100k prefix is also compared to
