@@ -103,38 +103,42 @@ static void run11(const char* name, Dev& d, const std::vector<uint32_t>& ref_len
 static const char* g_only = nullptr;  // run only the variant of this name (argv[3])
 
 template <int kMode, int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048,
-          int kCoop = 1, int kBlocksPerCu = 1, int kSched = 0>
+          int kCoop = 1, int kBlocksPerCu = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 0, int kPredSt = 1>
 static void run12(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                   const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
     if (g_only && strcmp(g_only, name) != 0) return;
     using G = Geo12<kWaves, kW, kO, kQ>;
-    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched>, 0, G::kBlock, kBlocksPerCu,
+    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt>, 0, G::kBlock, kBlocksPerCu,
                   d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
 // v12 diagnostic stamps (kMode 3): per wave total cycles, cycles in the decode phases, steps, fills
-template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048, int kSched = 0>
+template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048, int kSched = 0,
+          int kLongDyn = 1, int kDefer = 0, int kPredSt = 1>
 static void stamps12(const char* name, Dev& d, int num_cu) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     const size_t nw = (size_t)num_cu * kWaves;
     unsigned long long* dbg;
-    CK(hipMalloc(&dbg, nw * 4 * 8));
+    CK(hipMalloc(&dbg, nw * 16 * 8));
     DecodeArgs a = d.a;
     a.dbg = dbg;
-    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, 1, kSched>;
+    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, 1, kSched, kLongDyn, kDefer, kPredSt>;
     for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(num_cu), dim3(G::kBlock), 0, 0, a);
     CK(hipDeviceSynchronize());
-    std::vector<unsigned long long> h(nw * 4);
-    CK(hipMemcpy(h.data(), dbg, nw * 32, hipMemcpyDeviceToHost));
-    double s[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+    std::vector<unsigned long long> h(nw * 16);
+    CK(hipMemcpy(h.data(), dbg, nw * 128, hipMemcpyDeviceToHost));
+    double s[12] = {0}, mx[12] = {0};
     for (size_t w = 0; w < nw; ++w)
-        for (int j = 0; j < 4; ++j) {
-            s[j] += (double)h[w * 4 + j];
-            mx[j] = std::max(mx[j], (double)h[w * 4 + j]);
+        for (int j = 0; j < 12; ++j) {
+            s[j] += (double)h[w * 16 + j];
+            mx[j] = std::max(mx[j], (double)h[w * 16 + j]);
         }
     printf("{\"stamps\": \"%s\", \"cycles_mean\": %.0f, \"cycles_max\": %.0f, \"decode_cycles_mean\": %.0f, "
-           "\"decode_cycles_max\": %.0f, \"steps_mean\": %.1f, \"steps_max\": %.0f, \"barrier_wait_mean\": %.0f}\n",
-           name, s[0] / nw, mx[0], s[1] / nw, mx[1], s[2] / nw, mx[2], s[3] / nw);
+           "\"decode_cycles_max\": %.0f, \"steps_mean\": %.1f, \"steps_max\": %.0f, \"barrier_wait_mean\": %.0f, "
+           "\"pre_mean\": %.0f, \"setupA_mean\": %.0f, \"setupB_mean\": %.0f, \"long_mean\": %.0f, \"long_max\": %.0f, "
+           "\"setupA_fill0\": %.0f, \"setupB_fill0\": %.0f, \"byte_pass\": %.0f, \"last_flush\": %.0f}\n",
+           name, s[0] / nw, mx[0], s[1] / nw, mx[1], s[2] / nw, mx[2], s[3] / nw, s[4] / nw, s[5] / nw, s[6] / nw,
+           s[7] / nw, mx[7], s[8] / nw, s[9] / nw, s[10] / nw, s[11] / nw);
     fflush(stdout);
     CK(hipFree(dbg));
 }
@@ -213,9 +217,18 @@ int main(int argc, char** argv) {
         run12<4, 3, 2, false>("coop1_checked", d, ref_len, ref_st, ref_out, cu, 1);
         run12<0, 3, 2, false>("coop1", d, ref_len, ref_st, ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("coop1_snake", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 0>("snake_longstatic", d, ref_len, ref_st, ref_out, cu,
+                                                                   iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 1>("snake_defer", d, ref_len, ref_st, ref_out, cu,
+                                                                      iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 0>("snake_nopred", d, ref_len, ref_st, ref_out, cu,
+                                                                         iters);
+        run12<4, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1>("snake_pred_checked", d, ref_len, ref_st, ref_out,
+                                                                         cu, 1);
         if (!strcmp(g_only, "stamps")) {
             stamps12<2, 2, false, 16, 40960, 79104, 2048, 1>("coop1_snake", d, cu);
-            stamps12<3, 2, false>("coop1", d, cu);
+            stamps12<2, 2, false, 16, 40960, 79104, 2048, 1, 1, 0, 0>("snake_nopred", d, cu);
+            stamps12<2, 2, false, 16, 40960, 79104, 2048, 1, 0>("snake_longstatic", d, cu);
         }
         return 0;
     }

@@ -49,21 +49,11 @@ if mode == 4:
 if mode == 3:
     L = _lib.lib()
     L.hpk_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    buf = np.zeros(256 * 16 * 4, np.uint64)
+    buf = np.zeros(256 * 16 * 16, np.uint64)
     got = L.hpk_debug_stamps(buf.ctypes.data, buf.size)
-    st4 = buf[:got].reshape(-1, 4).astype(np.int64)
-    t0 = st4[:, 0].min()
-    start = (st4[:, 0] - t0) / 100.0  # s_memtime ticks at shader clock? report raw ticks too
-    staged = (st4[:, 1] - st4[:, 0])
-    total = (st4[:, 2] - st4[:, 0])
-    res["stamp_ticks"] = {
-        "start_spread": int(st4[:, 0].max() - t0),
-        "stage_med": int(np.median(staged)), "stage_max": int(staged.max()),
-        "total_med": int(np.median(total)), "total_p90": int(np.percentile(total, 90)), "total_max": int(total.max()),
-        "end_spread": int(st4[:, 2].max() - t0),
-        "xcc_counts": np.bincount((st4[:, 3] >> 32).astype(np.int64), minlength=8).tolist(),
-        "end_pct": [int(x) for x in np.percentile(st4[:, 2] - t0, [0, 10, 50, 90, 99, 100])],
-        "start_pct": [int(x) for x in np.percentile(st4[:, 0] - t0, [0, 10, 50, 90, 99, 100])],
-        "dur_by_wave_in_cu": [int(np.median(total[i::16])) for i in range(16)],
-    }
+    st8 = buf[:got].reshape(-1, 16).astype(np.int64)
+    names = ["total", "decode", "steps", "barrier_wait", "pre", "setupA", "setupB", "long", "setupA_fill0",
+             "setupB_fill0", "byte_pass", "last_flush"]
+    res["stamps_per_wave"] = {nm: {"mean": round(float(st8[:, i].mean()), 1), "max": int(st8[:, i].max())}
+                              for i, nm in enumerate(names)}
 print(json.dumps(res), flush=True)
