@@ -127,18 +127,20 @@ static void stamps12(const char* name, Dev& d, int num_cu) {
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nw * 16);
     CK(hipMemcpy(h.data(), dbg, nw * 128, hipMemcpyDeviceToHost));
-    double s[12] = {0}, mx[12] = {0};
+    double s[14] = {0}, mx[14] = {0};
     for (size_t w = 0; w < nw; ++w)
-        for (int j = 0; j < 12; ++j) {
+        for (int j = 0; j < 14; ++j) {
             s[j] += (double)h[w * 16 + j];
             mx[j] = std::max(mx[j], (double)h[w * 16 + j]);
         }
     printf("{\"stamps\": \"%s\", \"cycles_mean\": %.0f, \"cycles_max\": %.0f, \"decode_cycles_mean\": %.0f, "
            "\"decode_cycles_max\": %.0f, \"steps_mean\": %.1f, \"steps_max\": %.0f, \"barrier_wait_mean\": %.0f, "
            "\"pre_mean\": %.0f, \"setupA_mean\": %.0f, \"setupB_mean\": %.0f, \"long_mean\": %.0f, \"long_max\": %.0f, "
-           "\"setupA_fill0\": %.0f, \"setupB_fill0\": %.0f, \"byte_pass\": %.0f, \"last_flush\": %.0f}\n",
+           "\"setupA_fill0\": %.0f, \"setupB_fill0\": %.0f, \"byte_pass\": %.0f, \"last_flush\": %.0f, "
+           "\"long_literals\": %.0f, \"resync_rounds_per_long\": %.2f}\n",
            name, s[0] / nw, mx[0], s[1] / nw, mx[1], s[2] / nw, mx[2], s[3] / nw, s[4] / nw, s[5] / nw, s[6] / nw,
-           s[7] / nw, mx[7], s[8] / nw, s[9] / nw, s[10] / nw, s[11] / nw);
+           s[7] / nw, mx[7], s[8] / nw, s[9] / nw, s[10] / nw, s[11] / nw, s[13],
+           s[13] > 0 ? s[12] / s[13] : 0.0);
     fflush(stdout);
     CK(hipFree(dbg));
 }

@@ -4,7 +4,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.13 gfx950 decode v13 (alignbit step, two lookups per step, static snake schedule, cooperative long literals, LDS image)"
+#define HPK_VERSION "hpk 0.14 gfx950 decode v14 (alignbit step, two lookups per step, unconditional byte stores, static snake schedule, cooperative long literals with dynamic hand-out, LDS image); encode v2 (segmented scan, LDS image)"
 
 static thread_local std::string t_last_error;
 

@@ -77,6 +77,32 @@ __device__ __forceinline__ uint32_t win_at(const uint32_t* __restrict__ win32, u
     return __builtin_amdgcn_alignbit(q[-1], q[0], ~x);
 }
 
+// A window cursor for a walk: X = bit position + 31, the dword pair holding bit X - 31 and the dword
+// after it. The 32 bits at the position are one v_alignbit; an advance of <= 32 bits slides the pair
+// with the dword read ahead of the step (d3), so a lookup costs one LDS round trip, not three.
+struct WinCur {
+    uint32_t X, d0, d1, d2;
+};
+__device__ __forceinline__ void wc_load(WinCur& c, const uint32_t* __restrict__ win32, uint32_t p) {
+    c.X = p + 31u;
+    const uint32_t* q = win32 + (c.X >> 5);
+    c.d0 = q[-1];
+    c.d1 = q[0];
+    c.d2 = q[1];
+}
+__device__ __forceinline__ uint32_t wc_bits(const WinCur& c) { return __builtin_amdgcn_alignbit(c.d0, c.d1, ~c.X); }
+__device__ __forceinline__ uint32_t wc_next(const uint32_t* __restrict__ win32, const WinCur& c) {
+    return win32[(c.X >> 5) + 2];
+}
+__device__ __forceinline__ void wc_adv(WinCur& c, uint32_t n, uint32_t d3) {
+    const uint32_t xn = c.X + n;
+    const bool cross = (xn ^ c.X) > 31u;
+    c.d0 = cross ? c.d1 : c.d0;
+    c.d1 = cross ? c.d2 : c.d1;
+    c.d2 = cross ? d3 : c.d2;
+    c.X = xn;
+}
+
 // The codes one table entry decodes with rem bits left: ok1 / ok2 = its first / second code fits
 // inside the literal; returns the bits they use.
 __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
@@ -258,6 +284,8 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
     cnt = 0;
     stop = kThrough;
     bool run = pos < e;
+    WinCur c;
+    wc_load(c, win32, P0 + pos);
     // every pass advances >= 5 bits or stops; the guard only bounds the loop for the compiler and
     // any unforeseen input (a segment holds <= 8192 bits)
     for (uint32_t guard = 0; run; ++guard) {
@@ -265,11 +293,13 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
             stop = kStuck;
             break;
         }
-        const uint32_t w = win_at(win32, P0 + pos);
+        const uint32_t d3 = wc_next(win32, c);
+        const uint32_t w = wc_bits(c);
         const uint32_t rem = N - pos;
         const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
         bool a1, a2;
         lut12(e1, rem, a1, a2);
+        uint32_t adv = 0;
         if (a1) {
             const uint32_t l1 = (e1 >> 8) & 31u;
             if (kWrite) put8(out8, o + cnt, e1, oend, kStore);
@@ -277,11 +307,11 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
             if (a2 && pos + l1 < e) {  // the second code also starts inside the segment
                 if (kWrite) put8(out8, o + cnt, e1 >> 16, oend, kStore);
                 cnt += 1;
-                pos += (e1 >> 24) & 31u;
+                adv = (e1 >> 24) & 31u;
             } else {
-                pos += l1;
+                adv = l1;
             }
-            run = pos < e;
+            run = pos + adv < e;
         } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
             uint32_t s, len;
             bool eos;
@@ -295,13 +325,15 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
             } else {
                 if (kWrite) put8(out8, o + cnt, s, oend, kStore);
                 cnt += 1;
-                pos += len;
-                run = pos < e;
+                adv = len;
+                run = pos + adv < e;
             }
         } else {  // the next code does not fit: the literal ends here
             stop = kEnded;
             run = false;
         }
+        pos += adv;
+        wc_adv(c, adv, d3);
     }
     return pos;
 }
@@ -338,6 +370,8 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
         return false;
     };
     bool run = r.pos < e;
+    WinCur c;
+    wc_load(c, win32, P0 + b);
     for (uint32_t guard = 0; run; ++guard) {
         if (guard > 4096u) {
             r.stop = kStuck;
@@ -345,7 +379,8 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
         }
         if (join(r.pos)) break;
         const uint32_t pos = r.pos;
-        const uint32_t w = win_at(win32, P0 + pos);
+        const uint32_t d3 = wc_next(win32, c);
+        const uint32_t w = wc_bits(c);
         const uint32_t rem = N - pos;
         const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
         bool a1, a2;
@@ -379,6 +414,7 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
             r.stop = kEnded;
             run = false;
         }
+        wc_adv(c, r.pos - pos, d3);
     }
     return r;
 }
@@ -394,7 +430,8 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
 // first lane that does not come through holds the literal's true end.
 __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, int kStore,
-                                            uint32_t P0, uint32_t N, uint32_t o0, uint32_t& out_len, uint32_t& status) {
+                                            uint32_t P0, uint32_t N, uint32_t o0, uint32_t& out_len, uint32_t& status,
+                                            uint32_t& nround) {
     const uint32_t j = threadIdx.x & 63u;
     const uint32_t S = max(32u, (N + 63u) >> 6);
     const uint32_t s0 = j * S, e = (j + 1) * S;
@@ -413,7 +450,9 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
     walk(false);
     // lane j's start only changes after lane j-1's stopped changing, so 64 rounds always suffice
     bool stuck = false;
+    nround = 0;
     for (uint32_t round = 0;; ++round) {
+        nround = round;
         if (round > 64u) {
             stuck = true;
             break;
@@ -477,7 +516,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     const uint32_t dmy = (uint32_t)kImg + (threadIdx.x & 63u) * 4u;
     static_assert(kChunk >= 64, "a refill can hand out 64 slots");
     unsigned long long t_start = 0, t_dec = 0, n_steps = 0, n_fills = 0, t_pre = 0, t_setA = 0, t_setB = 0, t_long = 0,
-                       t_A0 = 0, t_B0 = 0, t_tail = 0, t_byte = 0;
+                       t_A0 = 0, t_B0 = 0, t_tail = 0, t_byte = 0, t_rounds = 0, n_longs = 0;
     if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
     __shared__ __attribute__((aligned(16))) uint8_t smem[G::kLdsBytes];
     uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
@@ -775,9 +814,13 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].x);
                     const uint32_t ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].y);
                     if (!(ey & kQ7Byte)) {  // (capacity below the bound: the byte pass below)
-                        uint32_t len, st;
+                        uint32_t len, st, nr;
                         long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
-                                    (ey >> 12) & 0x1FFFFu, len, st);
+                                    (ey >> 12) & 0x1FFFFu, len, st, nr);
+                        if (kMode == 3) {
+                            t_rounds += nr;
+                            n_longs += 1;
+                        }
                         if (lane == 0) s_lenst[ey & 0xFFFu] = len | (st << 24);
                     }
                     if (kLongDyn) {  // the next long literal: one LDS atomic per wave, read from lane 0
@@ -965,6 +1008,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         a.dbg[gwi * 16 + 9] = t_B0;
         a.dbg[gwi * 16 + 10] = t_byte;
         a.dbg[gwi * 16 + 11] = t_end - t_tail;
+        a.dbg[gwi * 16 + 12] = t_rounds;
+        a.dbg[gwi * 16 + 13] = n_longs;
     }
 }
 
