@@ -176,6 +176,25 @@ int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const uint8_t* b
                            uint32_t nblocks, hpk_blocks_out* out);
 void hpk_blocks_out_free(hpk_blocks_out* out);
 
+/* ---- HPACK header blocks: encode (the response path) ----------------------
+ * hpk_henc mirrors hpack::Encoder (crates/loona-hpack/src/encoder.rs:172-335): one per
+ * connection, holding the dynamic table, with the reference's single strategy (a header found
+ * whole in the table -> indexed; name found -> indexed name + literal value, not indexed; else a
+ * literal name + value with incremental indexing). String literals (encoder.rs:299-307): with
+ * huffman == 0 always raw, byte-identical to the reference; with huffman == 1 the H-bit form
+ * (RFC 7541 §5.2) whenever its Huffman encoding is strictly shorter than the raw bytes. */
+typedef struct hpk_henc hpk_henc;
+
+hpk_henc* hpk_henc_create(int huffman);                           /* Encoder::new(): max table 4096 */
+void hpk_henc_destroy(hpk_henc* enc);
+int hpk_henc_set_max_table_size(hpk_henc* enc, size_t max_size); /* encoder.rs:193-197 */
+/* Encoder::encode (encoder.rs:210-234) of n headers: header j's name is
+ * fields[field_off[2j] .. field_off[2j+1]) and its value fields[field_off[2j+1] .. field_off[2j+2]).
+ * Writes the block into out[0 .. cap) and its length to *out_len. Returns HPK_E_OK; HPK_E_NOSPACE
+ * with *out_len = the size needed and the encoder state unchanged; HPK_E_INVAL on bad arguments. */
+int hpk_henc_encode(hpk_henc* enc, const uint8_t* fields, const uint32_t* field_off, size_t n_headers, uint8_t* out,
+                    size_t cap, size_t* out_len);
+
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);
 

@@ -57,6 +57,10 @@ EXPORTS = (
     "hpk_hdec_table_size",
     "hpk_hdec_decode_blocks",
     "hpk_blocks_out_free",
+    "hpk_henc_create",
+    "hpk_henc_destroy",
+    "hpk_henc_set_max_table_size",
+    "hpk_henc_encode",
     "hpk_version",
 )
 
@@ -145,6 +149,15 @@ def lib() -> ctypes.CDLL:
         L.hpk_hdec_decode_blocks.restype = ctypes.c_int
         L.hpk_blocks_out_free.argtypes = [ctypes.POINTER(BlocksOut)]
         L.hpk_blocks_out_free.restype = None
+        L.hpk_henc_create.argtypes = [ctypes.c_int]
+        L.hpk_henc_create.restype = ctypes.c_void_p
+        L.hpk_henc_destroy.argtypes = [ctypes.c_void_p]
+        L.hpk_henc_destroy.restype = None
+        L.hpk_henc_set_max_table_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.hpk_henc_set_max_table_size.restype = ctypes.c_int
+        L.hpk_henc_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_size_t, c_sizep]
+        L.hpk_henc_encode.restype = ctypes.c_int
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

@@ -442,3 +442,143 @@ extern "C" void hpk_blocks_out_free(hpk_blocks_out* out) {
     free(out->blocks);
     memset(out, 0, sizeof *out);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Encoder (the response path): hpack::Encoder, crates/loona-hpack/src/encoder.rs:172-335, with
+// the H-bit rule as an option. The dynamic table is the reference's (lib.rs:43-164; the same
+// eviction as hpk_hdec), the lookup its find_header (lib.rs:261-288): static then dynamic
+// (newest first), the first full match, else the LAST name match.
+struct hpk_henc {
+    std::deque<std::pair<std::string, std::string>> table;  // front = newest
+    size_t size = 0;
+    size_t max_size = 4096;
+    int huffman = 0;
+
+    void consolidate() {
+        while (size > max_size) {
+            const auto& last = table.back();
+            size -= last.first.size() + last.second.size() + 32;
+            table.pop_back();
+        }
+    }
+    void add(std::string n, std::string v) {
+        size += n.size() + v.size() + 32;
+        table.emplace_front(std::move(n), std::move(v));
+        consolidate();
+    }
+    // 1-based index, 0 = no name match; *full = name and value matched
+    size_t find(const uint8_t* n, size_t nl, const uint8_t* v, size_t vl, bool* full) const {
+        size_t name_match = 0;
+        for (size_t i = 0; i < 61; ++i) {
+            const char* sn = kStatic[i][0];
+            if (strlen(sn) == nl && !memcmp(sn, n, nl)) {
+                const char* sv = kStatic[i][1];
+                if (strlen(sv) == vl && !memcmp(sv, v, vl)) {
+                    *full = true;
+                    return i + 1;
+                }
+                name_match = i + 1;
+            }
+        }
+        for (size_t j = 0; j < table.size(); ++j) {
+            const auto& e = table[j];
+            if (e.first.size() == nl && !memcmp(e.first.data(), n, nl)) {
+                if (e.second.size() == vl && !memcmp(e.second.data(), v, vl)) {
+                    *full = true;
+                    return 62 + j;
+                }
+                name_match = 62 + j;
+            }
+        }
+        *full = false;
+        return name_match;
+    }
+};
+
+namespace {
+
+// encode_integer_into (encoder.rs:93-122)
+void put_integer(std::vector<uint8_t>& o, size_t value, int prefix, uint8_t leading) {
+    const size_t mask = prefix >= 8 ? 0xFFu : ((1u << prefix) - 1u);
+    leading &= (uint8_t)~mask;
+    if (value < mask) {
+        o.push_back((uint8_t)(leading | value));
+        return;
+    }
+    o.push_back((uint8_t)(leading | mask));
+    value -= mask;
+    while (value >= 128) {
+        o.push_back((uint8_t)(value % 128 + 128));
+        value /= 128;
+    }
+    o.push_back((uint8_t)value);
+}
+
+// encode_string_literal (encoder.rs:299-307); with huffman, the H-bit form when strictly shorter
+void put_string(std::vector<uint8_t>& o, const uint8_t* s, size_t n, int huffman) {
+    if (huffman && n) {
+        const size_t hl = hpk_huffman_encoded_len(s, n);
+        if (hl < n) {
+            put_integer(o, hl, 7, 0x80);
+            const size_t at = o.size();
+            o.resize(at + hl);
+            size_t got = 0;
+            hpk_huffman_encode_one(s, n, o.data() + at, hl, &got);
+            return;
+        }
+    }
+    put_integer(o, n, 7, 0);
+    o.insert(o.end(), s, s + n);
+}
+
+}  // namespace
+
+extern "C" hpk_henc* hpk_henc_create(int huffman) {
+    hpk_henc* e = new (std::nothrow) hpk_henc();
+    if (e) e->huffman = huffman ? 1 : 0;
+    return e;
+}
+
+extern "C" void hpk_henc_destroy(hpk_henc* e) { delete e; }
+
+extern "C" int hpk_henc_set_max_table_size(hpk_henc* e, size_t n) {
+    if (!e) return HPK_E_INVAL;
+    e->max_size = n;
+    e->consolidate();
+    return HPK_E_OK;
+}
+
+extern "C" int hpk_henc_encode(hpk_henc* e, const uint8_t* fields, const uint32_t* field_off, size_t n, uint8_t* out,
+                               size_t cap, size_t* out_len) {
+    if (!e || !out_len || (n && !field_off) || (cap && !out)) return HPK_E_INVAL;
+    for (size_t k = 0; k < 2 * n; ++k)
+        if (field_off[k + 1] < field_off[k]) return HPK_E_INVAL;
+    if (n && field_off[2 * n] > field_off[0] && !fields) return HPK_E_INVAL;
+    // encode against a copy of the state; commit only when the block fits
+    hpk_henc next = *e;
+    std::vector<uint8_t> o;
+    for (size_t j = 0; j < n; ++j) {
+        const uint8_t* nm = fields + field_off[2 * j];
+        const size_t nl = field_off[2 * j + 1] - field_off[2 * j];
+        const uint8_t* v = fields + field_off[2 * j + 1];
+        const size_t vl = field_off[2 * j + 2] - field_off[2 * j + 1];
+        bool full = false;
+        const size_t idx = next.find(nm, nl, v, vl, &full);
+        if (idx == 0) {  // encode_literal with indexing (encoder.rs:279-291), then add_header
+            o.push_back(0x40);
+            put_string(o, nm, nl, next.huffman);
+            put_string(o, v, vl, next.huffman);
+            next.add(std::string((const char*)nm, nl), std::string((const char*)v, vl));
+        } else if (!full) {  // encode_indexed_name, not indexed (encoder.rs:311-323)
+            put_integer(o, idx, 4, 0x00);
+            put_string(o, v, vl, next.huffman);
+        } else {  // encode_indexed (encoder.rs:329-334)
+            put_integer(o, idx, 7, 0x80);
+        }
+    }
+    *out_len = o.size();
+    if (o.size() > cap) return HPK_E_NOSPACE;
+    if (!o.empty()) memcpy(out, o.data(), o.size());
+    *e = std::move(next);
+    return HPK_E_OK;
+}

@@ -1,4 +1,5 @@
-"""HPACK header-block decoding with batched Huffman strings.
+"""HPACK header blocks: decoding with batched Huffman strings and the response-path
+encoder (§8f-2).
 
 Mirrors loona-hpack's `hpack::Decoder` (crates/loona-hpack/src/decoder.rs:257-555):
 
@@ -19,6 +20,13 @@ decoder in order. Error values carry the reference's enum names:
     DecoderError("StringDecodingError", "NotEnoughOctets")
     DecoderError("StringDecodingError", ("HuffmanDecoderError", status))
     DecoderError("InvalidMaxDynamicSize"), DecoderError("SizeUpdateAtEnd")
+
+The encoder mirrors `hpack::Encoder` (crates/loona-hpack/src/encoder.rs:172-335):
+
+    e = Encoder()                       # Encoder::new(): raw string literals, as the reference
+    e = Encoder(huffman=True)           # the H-bit form whenever it is strictly shorter
+    e.set_max_table_size(256)           # encoder.rs:193-197
+    block = e.encode([(b"custom-key", b"custom-value")])   # encoder.rs:210-217
 """
 
 from __future__ import annotations
@@ -147,3 +155,46 @@ def decode_blocks(pairs, codec=None):
     """[(Decoder, block bytes)] -> [header list | DecoderError], all Huffman strings in one batch.
     The blocks of one decoder are applied in list order (connection order)."""
     return [hs if err is None else err for hs, err in _decode_raw(pairs, codec)]
+
+
+class Encoder:
+    """hpack::Encoder: one per connection (holds the dynamic table). huffman=False produces the
+    reference's bytes exactly; huffman=True Huffman-codes a string literal when that is shorter."""
+
+    def __init__(self, huffman: bool = False):
+        self._L = _lib.lib()
+        self._h = self._L.hpk_henc_create(1 if huffman else 0)
+        if not self._h:
+            raise MemoryError("hpk_henc_create")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._L.hpk_henc_destroy(h)
+
+    def set_max_table_size(self, n: int):
+        _lib.check(self._L.hpk_henc_set_max_table_size(self._h, n), "hpk_henc_set_max_table_size")
+
+    def encode(self, headers) -> bytes:
+        """encoder.rs:210-217: the header block for [(name, value)] (bytes)."""
+        parts, off = [], [0]
+        for name, value in headers:
+            for x in (name, value):
+                parts.append(bytes(x))
+                off.append(off[-1] + len(x))
+        if off[-1] >= 2**32:
+            raise ValueError("header fields of one block must stay below 4 GiB")
+        fields = np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8).copy()
+        off32 = np.asarray(off, dtype=np.uint32)
+        n = len(off) // 2
+        cap = 64 + 2 * off[-1] + 8 * n
+        while True:
+            out = np.empty(cap, np.uint8)
+            got = ctypes.c_size_t(0)
+            rc = self._L.hpk_henc_encode(self._h, fields.ctypes.data, off32.ctypes.data, n, out.ctypes.data, cap,
+                                         ctypes.byref(got))
+            if rc == -2:  # HPK_E_NOSPACE: state unchanged, retry with the size needed
+                cap = got.value
+                continue
+            _lib.check(rc, "hpk_henc_encode")
+            return out[: got.value].tobytes()

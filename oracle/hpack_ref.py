@@ -1,4 +1,5 @@
-"""TEST INFRASTRUCTURE ONLY — pure-Python restatement of loona-hpack's decode path.
+"""TEST INFRASTRUCTURE ONLY — pure-Python restatement of loona-hpack's decode path (and of its
+block encoder, encoder.rs, for the response-path tests).
 
 Used by tests/ (small cases) and tests/golden/make_golden.py as a second, independent checker
 next to the C oracle (hpk_oracle.c). Never imported by the product package ``loona_amd``.
@@ -234,6 +235,68 @@ class Decoder:
             i += consumed
         if last_was_size_update:
             raise DecoderError("SizeUpdateAtEnd")
+        return out
+
+
+def encode_integer(value: int, prefix: int, leading: int = 0) -> bytes:
+    """encode_integer_into (encoder.rs:93-122)."""
+    mask = 0xFF if prefix >= 8 else (1 << prefix) - 1
+    leading &= ~mask & 0xFF
+    if value < mask:
+        return bytes([leading | value])
+    out = [leading | mask]
+    value -= mask
+    while value >= 128:
+        out.append(value % 128 + 128)
+        value //= 128
+    out.append(value)
+    return bytes(out)
+
+
+class Encoder:
+    """Encoder (encoder.rs:172-335) with HeaderTable::find_header (lib.rs:261-288). huffman=True
+    adds this library's policy on top (not the reference's: encoder.rs:296-307 never Huffman-
+    codes): a string literal takes the H-bit form when its Huffman encoding is strictly shorter."""
+
+    def __init__(self, huffman=False):
+        global STATIC_TABLE
+        if STATIC_TABLE is None:
+            STATIC_TABLE = _load_static_table()
+        self.static = STATIC_TABLE
+        self.dynamic = DynamicTable()
+        self.huffman = huffman
+
+    def set_max_table_size(self, n):
+        self.dynamic.set_max_table_size(n)
+
+    def find_header(self, name, value):
+        matching = None
+        for i, (n, v) in enumerate(list(self.static) + list(self.dynamic.table)):
+            if n == name:
+                if v == value:
+                    return i + 1, True
+                matching = i + 1
+        return (matching, False) if matching is not None else None
+
+    def _string(self, s):
+        if self.huffman and s:
+            h = huffman_encode(s)
+            if len(h) < len(s):
+                return encode_integer(len(h), 7, 0x80) + h
+        return encode_integer(len(s), 7, 0) + s
+
+    def encode(self, headers):
+        out = b""
+        for name, value in headers:
+            name, value = bytes(name), bytes(value)
+            f = self.find_header(name, value)
+            if f is None:  # encode_literal(should_index = true) + add_header (encoder.rs:246-253)
+                out += bytes([0x40]) + self._string(name) + self._string(value)
+                self.dynamic.add_header(name, value)
+            elif not f[1]:  # encode_indexed_name(should_index = false) (encoder.rs:254-259, 311-323)
+                out += encode_integer(f[0], 4, 0) + self._string(value)
+            else:  # encode_indexed (encoder.rs:260-264, 329-334)
+                out += encode_integer(f[0], 7, 0x80)
         return out
 
 
