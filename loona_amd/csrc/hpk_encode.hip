@@ -197,23 +197,26 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             li = lo;
         }
         const bool f0 = any && S.ioff[li] == x0;  // the thread's first byte starts a literal
-        auto byte_at = [&](uint32_t j) -> uint32_t {  // input byte 32 * tid + j
-            const uint4 c = ch[j >> 4];
-            const uint32_t w = (j & 8u) ? ((j & 4u) ? c.w : c.z) : ((j & 4u) ? c.y : c.x);
-            return (w >> (8u * (j & 3u))) & 0xFFu;
-        };
+        // the thread's bytes by constant index (the loops below are unrolled: no register array
+        // indexed at run time, which the compiler would put in scratch memory)
+        const uint32_t wd[8] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y, ch[1].z, ch[1].w};
+        const uint32_t xt = tid * (uint32_t)kEBytes;
         // pass 1: (a literal starts in the thread's bytes, bits since the last start)
         uint32_t f = f0 ? 1u : 0u, v = 0;
         if (any) {
             uint32_t lj = li, nj = S.ioff[li + 1];
-            for (uint32_t x = x0; x < x1; ++x) {
-                while (x >= nj) {  // a literal starts at x (empty ones skipped)
-                    ++lj;
-                    nj = S.ioff[lj + 1];
-                    f = 1u;
-                    v = 0;
+#pragma unroll
+            for (int j = 0; j < kEBytes; ++j) {
+                const uint32_t x = xt + (uint32_t)j;
+                if (x >= x0 && x < x1) {
+                    while (x >= nj) {  // a literal starts at x (empty ones skipped)
+                        ++lj;
+                        nj = S.ioff[lj + 1];
+                        f = 1u;
+                        v = 0;
+                    }
+                    v += S.tab[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu].y;
                 }
-                v += S.tab[byte_at(x - tid * (uint32_t)kEBytes)].y;
             }
         }
         // segmented exclusive scan over the workgroup: the carry into each thread's first literal
@@ -244,23 +247,27 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             uint32_t lj = li, nj = S.ioff[li + 1];
             uint32_t bp = f0 ? 0u : carry;
             uint32_t ob = S.ooff[li] * 8u, cap = S.ooff[li + 1] * 8u - ob;
-            for (uint32_t x = x0; x < x1; ++x) {
-                while (x >= nj) {
-                    ++lj;
-                    nj = S.ioff[lj + 1];
-                    bp = 0;
-                    ob = S.ooff[lj] * 8u;
-                    cap = S.ooff[lj + 1] * 8u - ob;
+#pragma unroll
+            for (int j = 0; j < kEBytes; ++j) {
+                const uint32_t x = xt + (uint32_t)j;
+                if (x >= x0 && x < x1) {
+                    while (x >= nj) {
+                        ++lj;
+                        nj = S.ioff[lj + 1];
+                        bp = 0;
+                        ob = S.ooff[lj] * 8u;
+                        cap = S.ooff[lj + 1] * 8u - ob;
+                    }
+                    const uint2 e = S.tab[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+                    if (bp + e.y <= cap) {
+                        img_or(S.img, ob + bp, e.x, e.y);
+                    } else if (bp < cap) {  // overflow: the bits that still fit
+                        const uint32_t keep = cap - bp;
+                        img_or(S.img, ob + bp, e.x >> (e.y - keep), keep);
+                    }
+                    bp += e.y;
+                    if (x + 1 == nj) S.bits[lj] = bp;  // the literal's last byte
                 }
-                const uint2 e = S.tab[byte_at(x - tid * (uint32_t)kEBytes)];
-                if (bp + e.y <= cap) {
-                    img_or(S.img, ob + bp, e.x, e.y);
-                } else if (bp < cap) {  // overflow: the bits that still fit
-                    const uint32_t keep = cap - bp;
-                    img_or(S.img, ob + bp, e.x >> (e.y - keep), keep);
-                }
-                bp += e.y;
-                if (x + 1 == nj) S.bits[lj] = bp;  // the literal's last byte
             }
         }
         lds_barrier_e();
