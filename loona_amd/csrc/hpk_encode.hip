@@ -86,13 +86,13 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
 // ---------------------------------------------------------------------------------------------
 // v2
 
-constexpr int kEB = 1024;                 // threads per workgroup (16 waves)
-constexpr int kEBytes = 32;               // input bytes per thread per tile
-constexpr int kETile = kEB * kEBytes;     // 32 KiB of input per tile
-constexpr int kEO = 112 * 1024;           // LDS output image (bytes)
-constexpr int kEQ = 2048;                 // literals per tile
-constexpr int kEMeta = kEQ / kEB;         // offset rounds per thread
+// Geometry: kEB threads per workgroup, kEO bytes of LDS output image, kEQ literals per tile. The
+// product runs two workgroups of 512 threads per CU (16 KiB input tiles, 56 KiB images), so one
+// workgroup's global-memory waits overlap the other's LDS work; 1024 / 112 KiB / 2048 (one per CU)
+// stays for comparison (HPK_ENCODE_WIDE=1).
+constexpr int kEBytes = 32;  // input bytes per thread per tile
 
+template <int kEB, int kEO, int kEQ>
 struct EncLds {
     uint32_t img[kEO / 4];       // the tile's output span, big-endian dwords
     uint32_t ioff[kEQ + 1];      // input offsets of the tile's literals, relative to the tile base
@@ -104,7 +104,7 @@ struct EncLds {
     uint32_t wf[16], wv[16];     // per-wave scan totals
     uint32_t ctr[4];             // [0] literals in the tile
 };
-static_assert(sizeof(EncLds) <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+
 
 __device__ __forceinline__ void lds_barrier_e() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -119,8 +119,13 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
     }
 }
 
+template <int kEB, int kEO, int kEQ>
 __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
-    __shared__ __attribute__((aligned(16))) EncLds S;
+    constexpr int kETile = kEB * kEBytes;  // input bytes per tile
+    constexpr int kEMeta = kEQ / kEB;      // offset rounds per thread
+    static_assert(sizeof(EncLds<kEB, kEO, kEQ>) <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+    static_assert(kEB <= 1024 && kEQ % kEB == 0, "geometry");
+    __shared__ __attribute__((aligned(16))) EncLds<kEB, kEO, kEQ> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (tid < 256) {
         const uint32_t c = a.codes[tid], l = a.codes[257 + tid];
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     }
 }
 
-static int g_encode_v1 = -1;
+static int g_encode_v1 = -1, g_encode_wide = -1;
 
 }  // namespace
 
@@ -324,6 +329,8 @@ int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
     if (g_encode_v1 < 0) {
         const char* e = getenv("HPK_ENCODE_V1");
         g_encode_v1 = e && atoi(e) ? 1 : 0;
+        const char* w = getenv("HPK_ENCODE_WIDE");
+        g_encode_wide = w && atoi(w) ? 1 : 0;
     }
     EncodeArgs a{in_blob, in_off, n, out_blob, out_off, out_len, status, c->d_codes};
     const uintptr_t ip = (uintptr_t)in_blob, op = (uintptr_t)out_blob;
@@ -338,11 +345,15 @@ int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
         if (blocks < 1) blocks = 1;
         hipLaunchKernelGGL(hpk_encode_kernel, dim3((uint32_t)blocks), dim3(ENC_BLOCK), 0, c->stream, a);
     } else {
-        // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
+        // per = workgroups per CU; fewer when the batch is small (>= ~64 literals per workgroup)
+        const int per = g_encode_wide ? 1 : 2;
         uint64_t blocks = ((uint64_t)n + 63) / 64;
-        if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
+        if (blocks > (uint64_t)c->num_cu * per) blocks = (uint64_t)c->num_cu * per;
         if (blocks < 1) blocks = 1;
-        hipLaunchKernelGGL(hpk_encode2, dim3((uint32_t)blocks), dim3(kEB), 0, c->stream, a);
+        if (g_encode_wide)
+            hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048>), dim3((uint32_t)blocks), dim3(1024), 0, c->stream, a);
+        else
+            hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024>), dim3((uint32_t)blocks), dim3(512), 0, c->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
