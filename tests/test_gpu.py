@@ -176,6 +176,41 @@ def test_small_capacity_overflow(codec):
     assert (out[int(oo[-1]) :].cpu().numpy() == 0xAB).all()
 
 
+def test_exact_bound_regions(codec):
+    """Literals made only of 5-bit codes decode to exactly floor(8n/5) bytes: their output fills
+    the region's decoded bound, so a 16-bit store's second byte after the last symbol would fall
+    on the next region (the kernel repairs it, pair_fixup). Exact-bound regions back to back, with
+    exact (unrounded) capacities, empty literals and normal ones between them."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(17)
+    five = b"012aceiost"  # the 5-bit codes
+    lits = []
+    for k in range(6000):
+        r = k % 5
+        if r == 0:
+            lits.append(b"")
+        elif r == 4:
+            lits.append(huffman_encode(rng.choice(list(b"abcdefghij-/:"), int(rng.integers(1, 40))).astype(np.uint8).tobytes()))
+        else:
+            lits.append(huffman_encode(rng.choice(list(five), 8 * int(rng.integers(1, 12))).astype(np.uint8).tobytes()))
+    blob, off = pack(lits)
+    n = len(lits)
+    bound = (np.diff(off.astype(np.int64)) * 8) // 5
+    oo = np.zeros(n + 1, np.int64)
+    np.cumsum(bound, out=oo[1:])
+    dblob, doff = to_dev(blob), to_dev(off.astype(np.int32))
+    doo = to_dev(oo.astype(np.int32))
+    out = torch.full((int(oo[-1]) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    codec.decode_into(dblob, doff, out, doo, ol, st, device=True, sync=True)
+    got = (out.cpu().numpy(), oo.astype(np.uint32), ol.cpu().numpy().astype(np.uint32), st.cpu().numpy())
+    compare_batches(got, oracle_decode_batch(blob, off), "exact-bound regions")
+    assert (got[2].astype(np.int64)[1::5] == bound[1::5]).all()  # the 5-bit literals do fill their bound
+    assert (got[0][int(oo[-1]) :] == 0xAB).all()
+
+
 def test_encode_matches_oracle(codec):
     rng = np.random.default_rng(3)
     lens = rng.integers(0, 200, size=20000)
