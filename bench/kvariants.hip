@@ -9,7 +9,7 @@
 #include <algorithm>
 #include <vector>
 
-#include "../loona_amd/csrc/hpk_decode11.h"
+#include "legacy_decode11.h"
 #include "../loona_amd/csrc/hpk_decode12.h"
 
 using namespace hpkdec;

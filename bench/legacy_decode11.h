@@ -9,7 +9,7 @@
 // its own literal's dwords, which the L2 does not fully merge (PMC on v5: ~4x the output bytes
 // reach HBM), which is affordable while the kernel is far from the HBM roof.
 #pragma once
-#include "hpk_decode_kernel.h"
+#include "legacy_decode.h"
 
 namespace hpkdec {
 

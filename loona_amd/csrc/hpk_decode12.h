@@ -1,7 +1,7 @@
 // hpk_decode12.h — decode kernel v12: the v8 fill structure, a bit-position step, and a
 // wave-cooperative path for long literals.
 //
-// Fill structure as v8 (hpk_decode7 in hpk_decode_kernel.h): per fill an LDS input window, an LDS
+// Fill structure as v8 (hpk_decode7, now in bench/legacy_decode.h): per fill an LDS input window, an LDS
 // image of the fill's output span and a longest-first queue; the next fill's offsets and window
 // are prefetched into registers while the current one decodes, the previous image is written
 // back with 16-byte stores. What changes:
