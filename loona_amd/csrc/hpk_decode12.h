@@ -153,12 +153,16 @@ __device__ __forceinline__ void lit12_load(Lit12& L, const uint32_t* __restrict_
 
 // Append g (<= 4) bytes p (zero above them) to the pending output; store a dword when one is full.
 template <int kStore>
-__device__ __forceinline__ void acc_push(Lit12& L, uint32_t* __restrict__ out32, uint32_t p, uint32_t g) {
+__device__ __forceinline__ void acc_push(Lit12& L, uint32_t* __restrict__ out32, uint32_t p, uint32_t g,
+                                         uint32_t dmy32 = 0) {
     const uint64_t x = (uint64_t)p << (8u * L.accn);
     const uint32_t lo = L.acc | (uint32_t)x;
     const uint32_t n2 = L.accn + g;  // <= 7
     const bool full = n2 >= 4u;
-    if (full) put32(out32, L.o, lo, L.oend, kStore);
+    if (kStore == kPred)
+        out32[full ? L.o : dmy32] = lo;  // unconditional: a dword not yet complete goes to the dummy slot
+    else if (full)
+        put32(out32, L.o, lo, L.oend, kStore);
     L.o += full ? 1u : 0u;
     L.acc = full ? (uint32_t)(x >> 32) : lo;
     L.accn = n2 & 3u;
@@ -220,7 +224,7 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
         use += cont ? u2 : 0u;
         park |= cont & (e2 < HPK_LUT2_ONE) & (rem2 > (uint32_t)HPK_LUT_BITS);
     }
-    if (kAcc) acc_push<kStore>(L, out32, pk, g);
+    if (kAcc) acc_push<kStore>(L, out32, pk, g, dmy >> 2);
     const uint32_t xn = L.X + use;
     const bool cross = (xn ^ L.X) > 31u;
     L.d0 = cross ? L.d1 : L.d0;
@@ -242,7 +246,7 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
             L.Eb = L.X;
         } else {
             if (kAcc) {
-                acc_push<kStore>(L, out32, s, 1u);
+                acc_push<kStore>(L, out32, s, 1u, dmy >> 2);
             } else {
                 put8(out8, L.o, s, L.oend, kStore);
                 L.o += 1;
@@ -505,8 +509,13 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // kDefer: 1 = the previous fill's write-back stores are issued from registers during this fill's
 // decode, one slot per iteration; 0 = all of them between the two decodes.
 // kPredSt: 1 = lane steps store every byte unconditionally (kPred), 0 = exec-masked stores.
+// kSpread: 1 = the snake's queue slots interleaved over the waves and the lane phase before the
+// long literals (which waves then take dynamically); 0 = contiguous slots per wave, long first.
+// kSmallFill: a fill of at most this many literals also gives its literals of >= 64 encoded
+// bytes to whole waves (0 = only >= 224 bytes, always).
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
-          int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1>
+          int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1, int kSpread = 0,
+          int kSmallFill = 512>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -767,7 +776,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (pos[r] != 0xFFFFFFFFu) s_q[s_bbase[pos[r] >> 16] + (pos[r] & 0xFFFFu)] = make_uint2(ex[r], ey[r]);
-        const uint32_t nlong = kCoop ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_bbase[kLongBuckets]) : 0u;  // the queue's head: literals of >= 224 bytes
+        // the queue's head goes to whole waves: literals of >= 224 bytes; in a fill of few literals
+        // (long ones fill the window: lanes would idle) also those of >= 64 bytes (kSmallFill)
+        const uint32_t lb = (kSmallFill && k <= (uint32_t)kSmallFill) ? 32u : kLongBuckets;
+        const uint32_t nlong = kCoop ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_bbase[lb]) : 0u;
         // the next fill's offsets and window: in flight during this fill's decode. Unconditional
         // (clamped past the range end), so no register phi forces a wait on the stores below.
         const uint32_t cur_next = cur + k;
@@ -923,8 +935,11 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     T.prog = false;
                     lit12_load(T, win32);
                 };
-                load(L, tid);
-                const uint32_t t2 = 2u * G::kBlock - 1u - tid;
+                // kSpread: consecutive queue slots go to different waves (slot = lane * kWaves + wave),
+                // so a short lane queue (few literals below the long threshold) still reaches every wave
+                const uint32_t t1 = kSpread ? (tid & 63u) * (uint32_t)kWaves + (tid >> 6) : tid;
+                load(L, t1);
+                const uint32_t t2 = 2u * G::kBlock - 1u - t1;
                 bool nv = t2 < kl;  // a second literal is waiting in N
                 load(N, t2);
                 for (;;) {
@@ -959,6 +974,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             } else {
                 lane_phase(std::true_type{});
             }
+        } else if (kSpread) {  // lane literals first; waves then take long literals as they come free
+            lane_phase(std::false_type{});
+            long_phase();
         } else {
             long_phase();
             lane_phase(std::false_type{});
