@@ -432,6 +432,7 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
 // the lanes after it (a cascade of one lane per round); once corrected, the next lane re-walks
 // from the true start and, with the boundary mask, joins its old walk within a few codes. The
 // first lane that does not come through holds the literal's true end.
+template <uint32_t kLead>
 __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, int kStore,
                                             uint32_t P0, uint32_t N, uint32_t o0, uint32_t& out_len, uint32_t& status,
@@ -451,6 +452,39 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
             wk.pos = seg_walk<false>(win32, lut, lo, out8, kStore, P0, N, b, e, 0, 0, wk.cnt, wk.stop);
         }
     };
+    // lead-in: lane j > 0 first walks codes from kLead bits before its segment, so its speculative
+    // start is usually already the true one (Huffman walks fall into step within a few codes) and
+    // the rounds below mostly just confirm it instead of re-walking
+    if (kLead && j > 0 && s0 < N) {
+        uint32_t p = s0 > kLead ? s0 - kLead : 0u;
+        WinCur c;
+        wc_load(c, win32, P0 + p);
+        for (uint32_t g = 0; p < s0 && g < kLead; ++g) {
+            const uint32_t d3 = wc_next(win32, c);
+            const uint32_t w = wc_bits(c);
+            const uint32_t rem = N - p;
+            const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+            bool a1, a2;
+            lut12(e1, rem, a1, a2);
+            uint32_t adv = 0;
+            if (a1) {
+                const uint32_t l1 = (e1 >> 8) & 31u;
+                adv = (a2 && p + l1 < s0) ? (e1 >> 24) & 31u : l1;
+            } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
+                uint32_t sy, len;
+                bool eos;
+                lo_decode(w, lo, sy, len, eos);
+                if (len > rem || eos) break;
+                adv = len;
+            } else {
+                break;
+            }
+            p += adv;
+            wc_adv(c, adv, d3);
+        }
+        b = p >= s0 ? p : s0;  // a lead-in cut short leaves the plain speculative start
+        wk.pos = b;
+    }
     walk(false);
     // lane j's start only changes after lane j-1's stopped changing, so 64 rounds always suffice
     bool stuck = false;
@@ -513,9 +547,10 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // long literals (which waves then take dynamically); 0 = contiguous slots per wave, long first.
 // kSmallFill: a fill of at most this many literals also gives its literals of >= 64 encoded
 // bytes to whole waves (0 = only >= 224 bytes, always).
+// kLead: bits of lead-in walk before each speculative segment start of a long literal (0 = none).
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
           int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1, int kSpread = 0,
-          int kSmallFill = 512>
+          int kSmallFill = 512, uint32_t kLead = 0>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -827,7 +862,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     const uint32_t ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].y);
                     if (!(ey & kQ7Byte)) {  // (capacity below the bound: the byte pass below)
                         uint32_t len, st, nr;
-                        long_decode(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
+                        long_decode<kLead>(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
                                     (ey >> 12) & 0x1FFFFu, len, st, nr);
                         if (kMode == 3) {
                             t_rounds += nr;
