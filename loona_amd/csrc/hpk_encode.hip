@@ -138,15 +138,33 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     const uint32_t in_end = a.in_off[a.n] + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
     const uint4* g_in = reinterpret_cast<const uint4*>(a.in_base);
-    uint32_t cur = BA;
-    while (cur < BB) {  // block-uniform
-        const uint32_t cntl = min((uint32_t)kEQ, BB - cur);
-        const uint32_t gin = a.in_off[cur] + a.in_mis, gout = a.out_off[cur] + a.out_mis;
-        const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
-        // the tile's input chunks: in flight while the offsets are sorted out
-        uint4 ch[2];
+    // the next tile's input chunks and offsets are loaded into registers while the current one is
+    // encoded (issued before its write-back stores, so the wait for them does not include those)
+    uint4 ch[2];
+    uint32_t pi0[kEMeta], pi1[kEMeta], po0[kEMeta], po1[kEMeta];
+    auto prefetch = [&](uint32_t c, uint32_t base16) {
+        const uint32_t cn = min((uint32_t)kEQ, BB - c);
 #pragma unroll
         for (int r = 0; r < 2; ++r) ch[r] = g_in[min((base16 >> 4) + 2u * tid + (uint32_t)r, last16)];
+#pragma unroll
+        for (int r = 0; r < kEMeta; ++r) {
+            const uint32_t t = min(tid + (uint32_t)kEB * r, cn - 1u);
+            pi0[r] = a.in_off[c + t];
+            pi1[r] = a.in_off[c + t + 1];
+            po0[r] = a.out_off[c + t];
+            po1[r] = a.out_off[c + t + 1];
+        }
+    };
+    uint32_t cur = BA;
+    uint32_t gin = 0, gout = 0;  // the tile's input / output start (base-relative: + mis)
+    if (cur < BB) {
+        gin = a.in_off[cur] + a.in_mis;
+        gout = a.out_off[cur] + a.out_mis;
+        prefetch(cur, gin & ~15u);
+    }
+    while (cur < BB) {  // block-uniform
+        const uint32_t cntl = min((uint32_t)kEQ, BB - cur);
+        const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
         lds_barrier_e();  // the previous tile's image is out
         if (tid == 0) S.ctr[0] = 0;
         {  // clear the image
@@ -160,14 +178,9 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         for (int r = 0; r < kEMeta; ++r) {
             const uint32_t t = tid + (uint32_t)kEB * r;
             bool fits = false;
-            uint32_t i0 = 0, i1 = 0, o0 = 0, o1 = 0;
-            if (t < cntl) {
-                i0 = a.in_off[cur + t] + a.in_mis;
-                i1 = a.in_off[cur + t + 1] + a.in_mis;
-                o0 = a.out_off[cur + t] + a.out_mis;
-                o1 = a.out_off[cur + t + 1] + a.out_mis;
-                fits = i1 - base16 <= (uint32_t)kETile && o1 - ob16 <= (uint32_t)kEO;
-            }
+            const uint32_t i0 = pi0[r] + a.in_mis, i1 = pi1[r] + a.in_mis;
+            const uint32_t o0 = po0[r] + a.out_mis, o1 = po1[r] + a.out_mis;
+            if (t < cntl) fits = i1 - base16 <= (uint32_t)kETile && o1 - ob16 <= (uint32_t)kEO;
             if (fits) {
                 S.ioff[t] = i0 - base16;
                 S.ooff[t] = o0 - ob16;
@@ -178,13 +191,23 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             kw += (uint32_t)__popcll(__ballot(fits));
         }
         if (lane == 0 && kw) atomicAdd(&S.ctr[0], kw);
+        const uint4 chc0 = ch[0], chc1 = ch[1];
         lds_barrier_e();
         const uint32_t k = S.ctr[0];
         if (k == 0) {  // literal `cur` alone exceeds a tile: one lane, global memory
             if (tid == 0) encode_serial(a, S.code1, S.len1, cur);
             cur += 1;
+            if (cur < BB) {
+                gin = a.in_off[cur] + a.in_mis;
+                gout = a.out_off[cur] + a.out_mis;
+                prefetch(cur, gin & ~15u);
+            }
             continue;
         }
+        // the next tile: starts where this one ends
+        const uint32_t cur_n = cur + k;
+        const uint32_t gin_n = S.ioff[k] + base16, gout_n = S.ooff[k] + ob16;
+        if (cur_n < BB) prefetch(cur_n, gin_n & ~15u);
         const uint32_t xb = S.ioff[0], xe = S.ioff[k];  // the tile's input bytes [xb, xe)
         // this thread's bytes [x0, x1) and the literal holding x0
         const uint32_t x0 = max(tid * (uint32_t)kEBytes, xb), x1 = min(tid * (uint32_t)kEBytes + kEBytes, xe);
@@ -204,24 +227,35 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         const bool f0 = any && S.ioff[li] == x0;  // the thread's first byte starts a literal
         // the thread's bytes by constant index (the loops below are unrolled: no register array
         // indexed at run time, which the compiler would put in scratch memory)
-        const uint32_t wd[8] = {ch[0].x, ch[0].y, ch[0].z, ch[0].w, ch[1].x, ch[1].y, ch[1].z, ch[1].w};
+        const uint32_t wd[8] = {chc0.x, chc0.y, chc0.z, chc0.w, chc1.x, chc1.y, chc1.z, chc1.w};
         const uint32_t xt = tid * (uint32_t)kEBytes;
+        // the literal starts among the thread's bytes (bit j: byte xt + j starts a literal; empty
+        // literals add nothing) and the bytes it owns: masks, so the byte loops below have no
+        // control flow and their table reads issue back to back
+        uint32_t bm = 0, vm = 0, em = 0;  // em bit j: byte xt + j is the last of its literal
+        if (any) {
+            vm = (x1 - x0 == 32u ? 0xFFFFFFFFu : ((1u << (x1 - x0)) - 1u)) << (x0 - xt);
+            uint32_t lj = li + 1;
+            uint32_t nj = S.ioff[lj];
+            while (nj < x1) {
+                bm |= 1u << (nj - xt);
+                nj = S.ioff[++lj];
+            }
+            em = (bm >> 1) | (nj == x1 ? 1u << (x1 - 1u - xt) : 0u);
+        }
         // pass 1: (a literal starts in the thread's bytes, bits since the last start)
         uint32_t f = f0 ? 1u : 0u, v = 0;
-        if (any) {
-            uint32_t lj = li, nj = S.ioff[li + 1];
+#pragma unroll 1
+        for (uint32_t g = 0; g < (uint32_t)kEBytes / 8u; ++g) {  // 8 bytes at a time (register pressure)
+            const uint32_t lo8 = g == 0 ? wd[0] : g == 1 ? wd[2] : g == 2 ? wd[4] : wd[6];
+            const uint32_t hi8 = g == 0 ? wd[1] : g == 1 ? wd[3] : g == 2 ? wd[5] : wd[7];
+            const uint32_t vm8 = vm >> (8u * g), bm8 = bm >> (8u * g);
 #pragma unroll
-            for (int j = 0; j < kEBytes; ++j) {
-                const uint32_t x = xt + (uint32_t)j;
-                if (x >= x0 && x < x1) {
-                    while (x >= nj) {  // a literal starts at x (empty ones skipped)
-                        ++lj;
-                        nj = S.ioff[lj + 1];
-                        f = 1u;
-                        v = 0;
-                    }
-                    v += S.tab[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu].y;
-                }
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t ln = S.len1[((k < 4 ? lo8 : hi8) >> (8 * (k & 3))) & 0xFFu];
+                const bool ok = (vm8 >> k) & 1u, st = (bm8 >> k) & 1u;
+                f |= st ? 1u : 0u;
+                v = st ? ln : v + (ok ? ln : 0u);
             }
         }
         // segmented exclusive scan over the workgroup: the carry into each thread's first literal
@@ -247,33 +281,70 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             ev = 0;
         }
         const uint32_t carry = ef ? ev : cw + ev;
-        // pass 2: codes into the image, clipped at each literal's capacity
+        // pass 2: each run of codes (this thread's bytes of one literal) is packed into a 64-bit
+        // accumulator aligned to the image's dword grid: whole dwords inside the run are plain
+        // stores, the run's first and last (shared with neighbouring runs) are ds_or; a code past
+        // the literal's capacity is clipped (rare: the caller's capacity below the bound)
         if (any) {
-            uint32_t lj = li, nj = S.ioff[li + 1];
+            uint32_t lj = li;
             uint32_t bp = f0 ? 0u : carry;
             uint32_t ob = S.ooff[li] * 8u, cap = S.ooff[li + 1] * 8u - ob;
+            uint32_t dq = (ob + bp) >> 5, n = (ob + bp) & 31u;
+            uint64_t acc = 0;
+            bool first = true;
+            auto flush_run = [&]() {
+                if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
+                n = 0;
+                acc = 0;
+            };
+#pragma unroll 1
+            for (uint32_t g = 0; g < (uint32_t)kEBytes / 8u; ++g) {
+            const uint32_t lo8 = g == 0 ? wd[0] : g == 1 ? wd[2] : g == 2 ? wd[4] : wd[6];
+            const uint32_t hi8 = g == 0 ? wd[1] : g == 1 ? wd[3] : g == 2 ? wd[5] : wd[7];
+            const uint32_t vm8 = vm >> (8u * g), bm8 = bm >> (8u * g);
 #pragma unroll
-            for (int j = 0; j < kEBytes; ++j) {
-                const uint32_t x = xt + (uint32_t)j;
-                if (x >= x0 && x < x1) {
-                    while (x >= nj) {
-                        ++lj;
-                        nj = S.ioff[lj + 1];
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t b = ((k < 4 ? lo8 : hi8) >> (8 * (k & 3))) & 0xFFu;
+                const uint32_t code = S.code1[b], ln = S.len1[b];
+                if ((vm8 >> k) & 1u) {
+                    const uint32_t x = xt + 8u * g + (uint32_t)k;
+                    if ((bm8 >> k) & 1u) {  // a new literal: close the run, skip empty literals
+                        flush_run();
+                        while (S.ioff[lj + 1] <= x) ++lj;
                         bp = 0;
                         ob = S.ooff[lj] * 8u;
                         cap = S.ooff[lj + 1] * 8u - ob;
+                        dq = ob >> 5;
+                        n = ob & 31u;
+                        first = true;
                     }
-                    const uint2 e = S.tab[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-                    if (bp + e.y <= cap) {
-                        img_or(S.img, ob + bp, e.x, e.y);
-                    } else if (bp < cap) {  // overflow: the bits that still fit
-                        const uint32_t keep = cap - bp;
-                        img_or(S.img, ob + bp, e.x >> (e.y - keep), keep);
+                    if (bp + ln <= cap) {
+                        acc = (acc << ln) | code;
+                        n += ln;
+                        if (n >= 32u) {
+                            const uint32_t w = (uint32_t)(acc >> (n - 32u));
+                            if (first)
+                                atomicOr(&S.img[dq], w);
+                            else
+                                S.img[dq] = w;
+                            first = false;
+                            dq += 1;
+                            n -= 32u;
+                            acc &= (1ull << n) - 1ull;
+                        }
+                    } else {  // overflow: close the run, then the bits of this code that still fit
+                        flush_run();
+                        if (bp < cap) {
+                            const uint32_t keep = cap - bp;
+                            img_or(S.img, ob + bp, code >> (ln - keep), keep);
+                        }
                     }
-                    bp += e.y;
-                    if (x + 1 == nj) S.bits[lj] = bp;  // the literal's last byte
+                    bp += ln;
+                    if ((em >> (8u * g + k)) & 1u) S.bits[lj] = bp;  // the literal's last byte
                 }
             }
+            }
+            flush_run();
         }
         lds_barrier_e();
         // per literal: EOS padding, out_len, status
@@ -316,7 +387,9 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
                 }
             }
         }
-        cur += k;
+        cur = cur_n;
+        gin = gin_n;
+        gout = gout_n;
     }
 }
 
