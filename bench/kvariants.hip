@@ -104,18 +104,19 @@ static const char* g_only = nullptr;  // run only the variant of this name (argv
 
 template <int kMode, int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048,
           int kCoop = 1, int kBlocksPerCu = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 0, int kPredSt = 1,
-          int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0>
+          int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1>
 static void run12(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                   const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
     if (g_only && strcmp(g_only, name) != 0) return;
     using G = Geo12<kWaves, kW, kO, kQ>;
-    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead>, 0, G::kBlock, kBlocksPerCu,
+    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead, kEven>, 0, G::kBlock, kBlocksPerCu,
                   d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
 // v12 diagnostic stamps (kMode 3): per wave total cycles, cycles in the decode phases, steps, fills
 template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048, int kSched = 0,
-          int kLongDyn = 1, int kDefer = 0, int kPredSt = 1, int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0>
+          int kLongDyn = 1, int kDefer = 0, int kPredSt = 1, int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0,
+          int kEven = 1>
 static void stamps12(const char* name, Dev& d, int num_cu) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     const size_t nw = (size_t)num_cu * kWaves;
@@ -123,7 +124,7 @@ static void stamps12(const char* name, Dev& d, int num_cu) {
     CK(hipMalloc(&dbg, nw * 16 * 8));
     DecodeArgs a = d.a;
     a.dbg = dbg;
-    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, 1, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead>;
+    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, 1, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead, kEven>;
     for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(num_cu), dim3(G::kBlock), 0, 0, a);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nw * 16);
@@ -236,6 +237,17 @@ int main(int argc, char** argv) {
                                                                                cu, iters);
         run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1, 0, 512, 0>("snake_nolead", d, ref_len, ref_st,
                                                                                    ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1, 0, 512, 0, 0>("greedy", d, ref_len, ref_st, ref_out,
+                                                                                      cu, iters);
+        run12<0, 2, 2, false, 16, 36864, 83200, 2048, 1, 1, 1, 1, 0, 1, 0, 512, 0, 0>("w36_greedy", d, ref_len, ref_st,
+                                                                                      ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 43008, 77056, 2048, 1, 1, 1>("w42", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 45056, 75008, 2048, 1, 1, 1>("w44", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 38912, 81152, 2048, 1, 1, 1>("w38", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 36864, 83200, 2048, 1, 1, 1>("w36", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 34816, 85248, 2048, 1, 1, 1>("w34", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 32768, 87296, 2048, 1, 1, 1>("w32", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 28672, 91392, 2048, 1, 1, 1>("w28", d, ref_len, ref_st, ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1, 0, 512, 24>("snake_lead24", d, ref_len, ref_st,
                                                                                     ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1, 0, 512, 96>("snake_lead96", d, ref_len, ref_st,

@@ -4,7 +4,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.14 gfx950 decode v14 (alignbit step, two lookups per step, unconditional byte stores, static snake schedule, cooperative long literals with dynamic hand-out, LDS image); encode v2 (segmented scan, LDS image)"
+#define HPK_VERSION "hpk 0.16 gfx950 decode v16 (alignbit step, two lookups per step, unconditional byte stores, static snake schedule, equal-size fills, cooperative long literals with dynamic hand-out, LDS image); encode v2b (segmented scan, run accumulator, LDS image)"
 
 static thread_local std::string t_last_error;
 

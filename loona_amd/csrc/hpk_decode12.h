@@ -548,9 +548,10 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // kSmallFill: a fill of at most this many literals also gives its literals of >= 64 encoded
 // bytes to whole waves (0 = only >= 224 bytes, always).
 // kLead: bits of lead-in walk before each speculative segment start of a long literal (0 = none).
+// kEven: 1 = fills of about equal input size (fewest the window allows), 0 = greedy full windows.
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
           int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1, int kSpread = 0,
-          int kSmallFill = 512, uint32_t kLead = 0>
+          int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -590,6 +591,15 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     // last chunk holding a byte of THIS workgroup's literals: windows never read past it
     const uint32_t r_end = a.in_off[BB] + a.in_mis;
     const uint32_t rlast16 = r_end ? (r_end - 1) >> 4 : 0;
+    // kEven: the range is cut into the fewest fills the window allows, of about equal input size
+    // (a greedy cut leaves a small last fill that still costs a whole fill's setup, slowest literal
+    // and write-back); the effective window is that size plus a margin for literal granularity
+    uint32_t kWe = (uint32_t)kW;
+    if (kEven) {
+        const uint32_t R = r_end - ((a.in_off[BA] + a.in_mis) & ~15u);
+        const uint32_t nf = (R + (uint32_t)kW - 1u) / (uint32_t)kW;
+        if (nf > 1u) kWe = min((uint32_t)kW, (R + nf - 1u) / nf + 512u);
+    }
 
     // write back one decoded fill from the LDS image: the output span [G0, G1) with 16-byte
     // stores (bytewise in the two end chunks, which neighbours own), then out_len and status
@@ -732,7 +742,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
             const uint32_t o0 = P.oo0[r] + a.out_mis, o1 = P.oo1[r] + a.out_mis;
             // fitting literals form a prefix (offsets are non-decreasing)
-            const bool fits = t < cntl && p1 - base16 <= (uint32_t)kW && o1 - ob16 <= (uint32_t)kImg;
+            const bool fits = t < cntl && p1 - base16 <= kWe && o1 - ob16 <= (uint32_t)kImg;
             pos[r] = 0xFFFFFFFFu;
             if (fits) {
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
