@@ -242,6 +242,9 @@ int main(int argc, char** argv) {
         run12<0, 2, 2, false, 16, 36864, 83200, 2048, 1, 1, 1, 1, 0, 1, 0, 512, 0, 0>("w36_greedy", d, ref_len, ref_st,
                                                                                       ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 43008, 77056, 2048, 1, 1, 1>("w42", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 3, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("r3", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 1, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("r1", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 4, 2, false, 16, 40960, 79104, 2048, 1, 1, 1>("r4", d, ref_len, ref_st, ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 45056, 75008, 2048, 1, 1, 1>("w44", d, ref_len, ref_st, ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 38912, 81152, 2048, 1, 1, 1>("w38", d, ref_len, ref_st, ref_out, cu, iters);
         run12<0, 2, 2, false, 16, 36864, 83200, 2048, 1, 1, 1>("w36", d, ref_len, ref_st, ref_out, cu, iters);
