@@ -13,10 +13,13 @@
 //      emitted header list, reporting the FIRST error in field order exactly as the reference's
 //      single pass would (index integer, then name string or name index, then value string;
 //      Huffman status of a string where the reference would have decoded it).
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <deque>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -138,8 +141,8 @@ struct Field {
     Stage err_stage = kStIndex;
 };
 
-struct Scan {
-    std::vector<Field> fields;
+struct Scan {  // a block's fields: pools[pool][first .. first + n) (one field pool per host thread)
+    uint32_t pool = 0, first = 0, n = 0;
 };
 
 // decode_string's framing (decoder.rs:135-163) without the Huffman step.
@@ -156,8 +159,19 @@ int scan_string(const uint8_t* base, size_t pos, size_t end, Str* s, size_t* con
     return HPK_BLK_OK;
 }
 
-void scan_block(const uint8_t* base, size_t begin, size_t end, Scan* out, std::vector<uint32_t>* hoff,
-                std::vector<uint32_t>* hlen) {
+void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Field>* pool, std::vector<uint32_t>* hoff,
+                 std::vector<uint32_t>* hlen);
+
+void scan_block(const uint8_t* base, size_t begin, size_t end, uint32_t pool_id, std::vector<Field>* pool, Scan* out,
+                std::vector<uint32_t>* hoff, std::vector<uint32_t>* hlen) {
+    out->pool = pool_id;
+    out->first = (uint32_t)pool->size();
+    scan_fields(base, begin, end, pool, hoff, hlen);
+    out->n = (uint32_t)pool->size() - out->first;
+}
+
+void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Field>* pool, std::vector<uint32_t>* hoff,
+                 std::vector<uint32_t>* hlen) {
     size_t pos = begin;
     auto add_huff = [&](Str& s) {
         if (!s.huff) return;
@@ -172,7 +186,7 @@ void scan_block(const uint8_t* base, size_t begin, size_t end, Scan* out, std::v
         size_t c = 0;
         if (f.kind == kIndexed || f.kind == kSizeUpdate) {
             f.err = decode_integer(base + pos, end - pos, f.kind == kIndexed ? 7 : 5, &f.index, &c);
-            out->fields.push_back(f);
+            pool->push_back(f);
             if (f.err) return;
             pos += c;
             continue;
@@ -181,7 +195,7 @@ void scan_block(const uint8_t* base, size_t begin, size_t end, Scan* out, std::v
         const int prefix = f.kind == kLitIncr ? 6 : 4;
         f.err = decode_integer(base + pos, end - pos, prefix, &f.index, &c);
         if (f.err) {
-            out->fields.push_back(f);
+            pool->push_back(f);
             return;
         }
         size_t at = pos + c;
@@ -190,7 +204,7 @@ void scan_block(const uint8_t* base, size_t begin, size_t end, Scan* out, std::v
             f.err = scan_string(base, at, end, &f.name, &cn);
             if (f.err) {
                 f.err_stage = kStName;
-                out->fields.push_back(f);
+                pool->push_back(f);
                 return;
             }
             add_huff(f.name);
@@ -200,12 +214,12 @@ void scan_block(const uint8_t* base, size_t begin, size_t end, Scan* out, std::v
         f.err = scan_string(base, at, end, &f.value, &cv);
         if (f.err) {
             f.err_stage = kStValue;
-            out->fields.push_back(f);
+            pool->push_back(f);
             return;
         }
         add_huff(f.value);
         at += cv;
-        out->fields.push_back(f);
+        pool->push_back(f);
         pos = at;
     }
 }
@@ -302,7 +316,9 @@ struct Huff {
 };
 
 // Pass 3 for one block: the reference's single pass over the scanned fields.
-void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const Huff& h, Out& o, hpk_block_result* r) {
+void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const std::vector<std::vector<Field>>& pools,
+                 const Huff& h, Out& o, hpk_block_result* r) {
+    const Field* fields = pools[sc.pool].data() + sc.first;
     r->first_header = (uint32_t)o.headers.size();
     r->n_headers = 0;
     r->error = HPK_BLK_OK;
@@ -323,8 +339,8 @@ void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const Huff& h
     };
     auto huff_err = [&](const Str& s) -> int { return s.huff ? (*h.st)[s.lit] : 0; };
     bool last_was_size_update = false;
-    for (size_t fi = 0; fi < sc.fields.size(); ++fi) {
-        const Field& f = sc.fields[fi];
+    for (size_t fi = 0; fi < sc.n; ++fi) {
+        const Field& f = fields[fi];
         last_was_size_update = f.kind == kSizeUpdate;
         if (f.err && f.err_stage == kStIndex) return fail(f.err, 0);
         if (f.kind == kIndexed) {
@@ -380,32 +396,121 @@ void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const Huff& h
 
 }  // namespace
 
+namespace {
+// Scratch of hpk_hdec_decode_blocks, kept per calling thread (loona calls from its runtime
+// threads; each keeps its own): steady-state calls reuse capacity instead of page-faulting
+// fresh allocations in every pass.
+struct BlockScratch {
+    std::vector<Scan> scans;
+    std::vector<std::vector<Field>> pools;
+    std::vector<std::vector<uint32_t>> thoff, thlen;
+    std::vector<uint32_t> lbase, in_off, out_off, len, abase, hbase;
+    std::vector<uint8_t> st, in, dec, owner;
+    std::vector<Out> outs;
+};
+thread_local BlockScratch t_scratch;
+}  // namespace
+
 extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const uint8_t* blocks,
                                       const uint32_t* block_off, uint32_t nblocks, hpk_blocks_out* out) {
     if (!decs || !block_off || !out || (nblocks && block_off[nblocks] && !blocks)) return HPK_E_INVAL;
     memset(out, 0, sizeof *out);
     for (uint32_t b = 0; b < nblocks; ++b)
         if (!decs[b] || block_off[b + 1] < block_off[b]) return HPK_E_INVAL;
-    // pass 1: scan every block, gather the Huffman strings
-    std::vector<Scan> scans(nblocks);
-    std::vector<uint32_t> hoff, hlen;
-    for (uint32_t b = 0; b < nblocks; ++b) scan_block(blocks, block_off[b], block_off[b + 1], &scans[b], &hoff, &hlen);
-    // pass 2: one batch for all of them
-    const uint32_t n = (uint32_t)hoff.size();
-    std::vector<uint32_t> in_off(n + 1), out_off(n + 1), len(n ? n : 1);
-    std::vector<uint8_t> st(n ? n : 1);
-    size_t tot = 0, otot = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        in_off[i] = (uint32_t)tot;
-        out_off[i] = (uint32_t)otot;
-        tot += hlen[i];
-        otot += ((hpk_decoded_bound(hlen[i]) + 3) & ~(size_t)3);
-        if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
+    // Host threads: blocks are independent in pass 1; in pass 3 a decoder's blocks stay on one
+    // thread, in order (decoders are independent of each other). Per-thread outputs are joined
+    // at the end (a block's headers stay contiguous; blocks need not be in order in the arrays).
+    int nth = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("HPK_HDEC_THREADS")) nth = atoi(e);  // (for measurements)
+    if (nth > 16) nth = 16;
+    if (nth < 1) nth = 1;
+    if ((uint32_t)nth > nblocks / 256u + 1u) nth = (int)(nblocks / 256u + 1u);
+    auto parallel = [&](auto fn) {  // fn(thread index)
+        if (nth == 1) {
+            fn(0);
+            return;
+        }
+        std::vector<std::thread> th;
+        for (int t = 1; t < nth; ++t) th.emplace_back(fn, t);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+    static const bool timing = getenv("HPK_HDEC_TIMING") != nullptr;  // per-pass wall times to stderr
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_0 = now();
+    auto us = [&](std::chrono::steady_clock::time_point a) {
+        return (long)std::chrono::duration_cast<std::chrono::microseconds>(now() - a).count();
+    };
+    // pass 1: scan every block, gather the Huffman strings (contiguous block ranges per thread)
+    BlockScratch& W = t_scratch;
+    std::vector<Scan>& scans = W.scans;
+    scans.resize(nblocks);
+    std::vector<std::vector<Field>>& pools = W.pools;
+    std::vector<std::vector<uint32_t>>&thoff = W.thoff, &thlen = W.thlen;
+    if ((int)pools.size() < nth) {
+        pools.resize(nth);
+        thoff.resize(nth);
+        thlen.resize(nth);
+        W.outs.resize(nth);
     }
+    auto blk0 = [&](int t) { return (uint32_t)((uint64_t)nblocks * t / nth); };
+    parallel([&](int t) {
+        // the vectors are moved into locals while the thread appends: their headers sit next to
+        // the other threads' in the scratch arrays (false sharing on every push_back otherwise)
+        const size_t bytes = block_off[blk0(t + 1)] - block_off[blk0(t)];
+        std::vector<Field> pool = std::move(pools[t]);
+        std::vector<uint32_t> ho = std::move(thoff[t]), hl = std::move(thlen[t]);
+        pool.clear();
+        ho.clear();
+        hl.clear();
+        pool.reserve(bytes / 8 + 16);  // ~12 block bytes per field on the interop corpus
+        ho.reserve(bytes / 8 + 16);
+        hl.reserve(bytes / 8 + 16);
+        for (uint32_t b = blk0(t); b < blk0(t + 1); ++b)
+            scan_block(blocks, block_off[b], block_off[b + 1], (uint32_t)t, &pool, &scans[b], &ho, &hl);
+        pools[t] = std::move(pool);
+        thoff[t] = std::move(ho);
+        thlen[t] = std::move(hl);
+    });
+    std::vector<uint32_t>& lbase = W.lbase;  // each thread's first index in the batch
+    lbase.assign(nth + 1, 0);
+    for (int t = 0; t < nth; ++t) lbase[t + 1] = lbase[t] + (uint32_t)thoff[t].size();
+    parallel([&](int t) {  // local Huffman indices -> batch indices
+        if (!lbase[t]) return;
+        for (Field& f : pools[t]) {
+            if (f.name.huff) f.name.lit += lbase[t];
+            if (f.value.huff) f.value.lit += lbase[t];
+        }
+    });
+    const long us_scan = us(t_0);
+    auto t_1 = now();
+    // pass 2: one batch for all of them
+    const uint32_t n = lbase[nth];
+    std::vector<uint32_t>&in_off = W.in_off, &out_off = W.out_off, &len = W.len;
+    std::vector<uint8_t>& st = W.st;
+    in_off.resize(n + 1);
+    out_off.resize(n + 1);
+    len.resize(n ? n : 1);
+    st.resize(n ? n : 1);
+    size_t tot = 0, otot = 0;
+    for (int t = 0; t < nth; ++t)
+        for (size_t j = 0; j < thlen[t].size(); ++j) {
+            const uint32_t i = lbase[t] + (uint32_t)j;
+            in_off[i] = (uint32_t)tot;
+            out_off[i] = (uint32_t)otot;
+            tot += thlen[t][j];
+            otot += ((hpk_decoded_bound(thlen[t][j]) + 3) & ~(size_t)3);
+            if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
+        }
     in_off[n] = (uint32_t)tot;
     out_off[n] = (uint32_t)otot;
-    std::vector<uint8_t> in(tot ? tot : 1), dec(otot ? otot : 1);
-    for (uint32_t i = 0; i < n; ++i) memcpy(in.data() + in_off[i], blocks + hoff[i], hlen[i]);
+    std::vector<uint8_t>&in = W.in, &dec = W.dec;
+    in.resize(tot ? tot : 1);
+    dec.resize(otot ? otot : 1);
+    parallel([&](int t) {
+        for (size_t j = 0; j < thoff[t].size(); ++j)
+            memcpy(in.data() + in_off[lbase[t] + j], blocks + thoff[t][j], thlen[t][j]);
+    });
     if (n) {
         const int rc = ctx ? hpk_decode_batch(ctx, in.data(), in_off.data(), n, dec.data(), out_off.data(), len.data(),
                                               st.data(), HPK_PTR_HOST)
@@ -413,25 +518,64 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
                                                   st.data(), 0);
         if (rc) return rc;
     }
-    // pass 3: apply in block order (the blocks of one decoder are in connection order)
-    Out o;
-    std::vector<hpk_block_result> res(nblocks);
-    const Huff h{&dec, &out_off, &len, &st};
-    for (uint32_t b = 0; b < nblocks; ++b) apply_block(decs[b], blocks, scans[b], h, o, &res[b]);
-    // hand the results over in malloc'd buffers (hpk_blocks_out_free)
-    out->arena_len = o.arena.size();
-    out->n_headers = o.headers.size();
+    const long us_batch = us(t_1);
+    auto t_2 = now();
+    // pass 3: apply; thread of a decoder = a hash of its address, its blocks in list order
+    std::vector<Out>& outs = W.outs;
+    for (int t = 0; t < nth; ++t) {  // decoded headers take a few times the block bytes
+        outs[t].arena.clear();
+        outs[t].headers.clear();
+        outs[t].arena.reserve(4 * (size_t)block_off[nblocks] / (size_t)nth + 4096);
+        outs[t].headers.reserve(pools[t].size() + 16);
+    }
+    // results go straight into the caller's malloc'd buffers (hpk_blocks_out_free)
     out->n_blocks = nblocks;
-    out->arena = (uint8_t*)malloc(o.arena.size() ? o.arena.size() : 1);
-    out->headers = (hpk_header*)malloc((o.headers.size() ? o.headers.size() : 1) * sizeof(hpk_header));
     out->blocks = (hpk_block_result*)malloc((nblocks ? nblocks : 1) * sizeof(hpk_block_result));
-    if (!out->arena || !out->headers || !out->blocks) {
+    if (!out->blocks) return HPK_E_INVAL;
+    hpk_block_result* res = out->blocks;
+    std::vector<uint8_t>& owner = W.owner;
+    owner.resize(nblocks);
+    for (uint32_t b = 0; b < nblocks; ++b)
+        owner[b] = (uint8_t)(((uintptr_t)decs[b] >> 4) * 0x9E3779B97F4A7C15ull >> 59) % (uint32_t)nth;
+    const Huff h{&dec, &out_off, &len, &st};
+    parallel([&](int t) {
+        Out mine = std::move(outs[t]);  // (a local: no false sharing with the neighbours' headers)
+        for (uint32_t b = 0; b < nblocks; ++b)
+            if (owner[b] == t) apply_block(decs[b], blocks, scans[b], pools, h, mine, &res[b]);
+        outs[t] = std::move(mine);
+    });
+    // join the per-thread outputs into the caller's buffers
+    std::vector<uint32_t>&abase = W.abase, &hbase = W.hbase;
+    abase.assign(nth, 0);
+    hbase.assign(nth, 0);
+    size_t at = 0, ht = 0;
+    for (int t = 0; t < nth; ++t) {
+        abase[t] = (uint32_t)at;
+        hbase[t] = (uint32_t)ht;
+        at += outs[t].arena.size();
+        ht += outs[t].headers.size();
+    }
+    out->arena_len = at;
+    out->n_headers = ht;
+    out->arena = (uint8_t*)malloc(at ? at : 1);
+    out->headers = (hpk_header*)malloc((ht ? ht : 1) * sizeof(hpk_header));
+    if (at >= (1ull << 32) || !out->arena || !out->headers) {
         hpk_blocks_out_free(out);
         return HPK_E_INVAL;
     }
-    if (!o.arena.empty()) memcpy(out->arena, o.arena.data(), o.arena.size());
-    if (!o.headers.empty()) memcpy(out->headers, o.headers.data(), o.headers.size() * sizeof(hpk_header));
-    if (nblocks) memcpy(out->blocks, res.data(), nblocks * sizeof(hpk_block_result));
+    parallel([&](int t) {
+        if (!outs[t].arena.empty()) memcpy(out->arena + abase[t], outs[t].arena.data(), outs[t].arena.size());
+        for (size_t j = 0; j < outs[t].headers.size(); ++j) {
+            hpk_header hd = outs[t].headers[j];
+            hd.name_off += abase[t];
+            hd.value_off += abase[t];
+            out->headers[hbase[t] + j] = hd;
+        }
+    });
+    for (uint32_t b = 0; b < nblocks; ++b) res[b].first_header += hbase[owner[b]];
+    if (timing)
+        fprintf(stderr, "hpk_hdec_decode_blocks: %d threads, scan %ld us, batch %ld us, apply+join %ld us\n", nth,
+                us_scan, us_batch, us(t_2));
     return HPK_E_OK;
 }
 

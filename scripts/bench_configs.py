@@ -148,18 +148,19 @@ def config4(codec):
     off32 = off.astype(np.uint32)
     res = {}
     for leg, ctx in (("device", codec._h), ("cpu_batch", None)):
-        decs = [L.hpk_hdec_create() for _ in range(nconn)]
-        arr = (ctypes.c_void_p * len(blocks))(*[decs[o] for o in owners])
-        out = _lib.BlocksOut()
-        t0 = time.perf_counter()
-        rc = L.hpk_hdec_decode_blocks(ctx, arr, blob.ctypes.data, off32.ctypes.data, len(blocks), ctypes.byref(out))
-        dt = time.perf_counter() - t0
-        _lib.check(rc, "hpk_hdec_decode_blocks")
-        errs = sum(1 for b in range(len(blocks)) if out.blocks[b].error)
-        nh = out.n_headers
-        L.hpk_blocks_out_free(ctypes.byref(out))
-        for d in decs:
-            L.hpk_hdec_destroy(d)
+        for rep in range(2):  # the first call grows the context's scratch buffers: time the second
+            decs = [L.hpk_hdec_create() for _ in range(nconn)]
+            arr = (ctypes.c_void_p * len(blocks))(*[decs[o] for o in owners])
+            out = _lib.BlocksOut()
+            t0 = time.perf_counter()
+            rc = L.hpk_hdec_decode_blocks(ctx, arr, blob.ctypes.data, off32.ctypes.data, len(blocks), ctypes.byref(out))
+            dt = time.perf_counter() - t0
+            _lib.check(rc, "hpk_hdec_decode_blocks")
+            errs = sum(1 for b in range(len(blocks)) if out.blocks[b].error)
+            nh = out.n_headers
+            L.hpk_blocks_out_free(ctypes.byref(out))
+            for d in decs:
+                L.hpk_hdec_destroy(d)
         res[leg] = (dt, errs, nh)
     lit_bytes = sum(len(x) for x in interop_literals()) * reps
     emit({"config": "config4", "source": "crates/loona-hpack/fixtures/hpack/interop (5 encoders' captured blocks)",
