@@ -89,8 +89,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
 // Geometry: kEB threads per workgroup, kEO bytes of LDS output image, kEQ literals per tile. The
 // product runs two workgroups of 512 threads per CU (16 KiB input tiles, 56 KiB images), so one
 // workgroup's global-memory waits overlap the other's LDS work; 1024 / 112 KiB / 2048 (one per CU)
-// stays for comparison (HPK_ENCODE_WIDE=1).
-constexpr int kEBytes = 32;  // input bytes per thread per tile
+// stays for comparison (HPK_ENCODE_CFG=1; 2 and 3: 16 bytes per thread).
 
 template <int kEB, int kEO, int kEQ>
 struct EncLds {
@@ -119,8 +118,10 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
     }
 }
 
-template <int kEB, int kEO, int kEQ>
+template <int kEB, int kEO, int kEQ, int kEBytes = 32>  // kEBytes: input bytes per thread per tile (16 or 32)
 __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
+    static_assert(kEBytes == 16 || kEBytes == 32, "bytes per thread");
+    constexpr int kCh = kEBytes / 16;  // 16-byte chunks per thread
     constexpr int kETile = kEB * kEBytes;  // input bytes per tile
     constexpr int kEMeta = kEQ / kEB;      // offset rounds per thread
     static_assert(sizeof(EncLds<kEB, kEO, kEQ>) <= 163840, "LDS budget (160 KiB per CU on gfx950)");
@@ -140,12 +141,12 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     const uint4* g_in = reinterpret_cast<const uint4*>(a.in_base);
     // the next tile's input chunks and offsets are loaded into registers while the current one is
     // encoded (issued before its write-back stores, so the wait for them does not include those)
-    uint4 ch[2];
+    uint4 ch[2] = {};
     uint32_t pi0[kEMeta], pi1[kEMeta], po0[kEMeta], po1[kEMeta];
     auto prefetch = [&](uint32_t c, uint32_t base16) {
         const uint32_t cn = min((uint32_t)kEQ, BB - c);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) ch[r] = g_in[min((base16 >> 4) + 2u * tid + (uint32_t)r, last16)];
+        for (int r = 0; r < kCh; ++r) ch[r] = g_in[min((base16 >> 4) + (uint32_t)kCh * tid + (uint32_t)r, last16)];
 #pragma unroll
         for (int r = 0; r < kEMeta; ++r) {
             const uint32_t t = min(tid + (uint32_t)kEB * r, cn - 1u);
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         // control flow and their table reads issue back to back
         uint32_t bm = 0, vm = 0, em = 0;  // em bit j: byte xt + j is the last of its literal
         if (any) {
-            vm = (x1 - x0 == 32u ? 0xFFFFFFFFu : ((1u << (x1 - x0)) - 1u)) << (x0 - xt);
+            vm = (uint32_t)(((1ull << (x1 - x0)) - 1ull) << (x0 - xt));
             uint32_t lj = li + 1;
             uint32_t nj = S.ioff[lj];
             while (nj < x1) {
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     }
 }
 
-static int g_encode_v1 = -1, g_encode_wide = -1;
+static int g_encode_v1 = -1, g_encode_cfg = 0;
 
 }  // namespace
 
@@ -402,8 +403,8 @@ int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
     if (g_encode_v1 < 0) {
         const char* e = getenv("HPK_ENCODE_V1");
         g_encode_v1 = e && atoi(e) ? 1 : 0;
-        const char* w = getenv("HPK_ENCODE_WIDE");
-        g_encode_wide = w && atoi(w) ? 1 : 0;
+        const char* w = getenv("HPK_ENCODE_CFG");  // geometry variants for measurements (0 = product)
+        g_encode_cfg = w ? atoi(w) : 0;
     }
     EncodeArgs a{in_blob, in_off, n, out_blob, out_off, out_len, status, c->d_codes};
     const uintptr_t ip = (uintptr_t)in_blob, op = (uintptr_t)out_blob;
@@ -419,14 +420,24 @@ int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
         hipLaunchKernelGGL(hpk_encode_kernel, dim3((uint32_t)blocks), dim3(ENC_BLOCK), 0, c->stream, a);
     } else {
         // per = workgroups per CU; fewer when the batch is small (>= ~64 literals per workgroup)
-        const int per = g_encode_wide ? 1 : 2;
+        const int per = (g_encode_cfg == 1 || g_encode_cfg == 2) ? 1 : 2;
         uint64_t blocks = ((uint64_t)n + 63) / 64;
         if (blocks > (uint64_t)c->num_cu * per) blocks = (uint64_t)c->num_cu * per;
         if (blocks < 1) blocks = 1;
-        if (g_encode_wide)
-            hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048>), dim3((uint32_t)blocks), dim3(1024), 0, c->stream, a);
-        else
-            hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024>), dim3((uint32_t)blocks), dim3(512), 0, c->stream, a);
+        const dim3 grid((uint32_t)blocks);
+        switch (g_encode_cfg) {
+            case 1:  // one 1024-thread workgroup per CU, 32 KiB tiles
+                hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 32>), grid, dim3(1024), 0, c->stream, a);
+                break;
+            case 2:  // one 1024-thread workgroup per CU, 16 bytes per thread
+                hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 16>), grid, dim3(1024), 0, c->stream, a);
+                break;
+            case 3:  // two 512-thread workgroups per CU, 16 bytes per thread
+                hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 16>), grid, dim3(512), 0, c->stream, a);
+                break;
+            default:  // product: two 512-thread workgroups per CU, 32 bytes per thread
+                hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 32>), grid, dim3(512), 0, c->stream, a);
+        }
     }
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
