@@ -186,6 +186,12 @@ class Decoder:
         self.dynamic = DynamicTable()
         self.max_allowed_table_size = None
 
+    def set_max_table_size(self, n):
+        """Decoder::set_max_table_size (decoder.rs:325-340); the allowed-size assert is a panic
+        there, so it is only restated for the unset case the tests use."""
+        assert self.max_allowed_table_size is None or n <= self.max_allowed_table_size
+        self.dynamic.set_max_table_size(n)
+
     def get_from_table(self, index):
         if index == 0:
             raise DecoderError("HeaderIndexOutOfBounds")

@@ -139,3 +139,40 @@ def test_random_blocks_match_restatement():
     assert len(kinds) >= 5
     for i, (g, w) in enumerate(zip(got, want)):
         assert g == w, (i, pairs[i][1].hex())
+
+
+def test_httpwg_invalid_header_block_fragment():
+    """httpwg's `invalid_header_block_fragment` (crates/httpwg/src/rfc9113/_4_http_frames.rs:153-170)
+    sends the block b"\\x40" (literal with incremental indexing, no name length) and expects
+    COMPRESSION_ERROR, which loona raises for any DecoderError (h2/server.rs:1621-1634,
+    h2/types.rs:366-367). The error itself must equal decoder.rs's."""
+    want = _ref_decode(hpack_ref.Decoder(), b"\x40")
+    assert isinstance(want, hpack.DecoderError)
+    with pytest.raises(hpack.DecoderError) as ei:
+        hpack.Decoder().decode(b"\x40")
+    assert ei.value == want
+    assert hpack.decode_blocks([(hpack.Decoder(), b"\x40")]) == [want]
+
+
+def test_every_truncation_of_rfc_blocks():
+    """Every proper prefix of every RFC 7541 App. C block, decoded with the table state the
+    sequence had built so far: headers or the first error equal the restatement's."""
+    g = load("rfc7541_blocks.json")
+    pairs, want = [], []
+    for seq in g["sequences"]:
+        for k, b in enumerate(seq["blocks"]):
+            w = bytes.fromhex(b["wire"])
+            for cut in range(len(w)):
+                d, r = hpack.Decoder(), hpack_ref.Decoder()
+                if seq["max_table_size"] is not None:
+                    d.set_max_table_size(seq["max_table_size"])
+                    r.set_max_table_size(seq["max_table_size"])
+                for prev in seq["blocks"][:k]:
+                    d.decode(bytes.fromhex(prev["wire"]))
+                    r.decode(bytes.fromhex(prev["wire"]))
+                pairs.append((d, w[:cut]))
+                want.append(_ref_decode(r, w[:cut]))
+    got = hpack.decode_blocks(pairs)
+    assert sum(isinstance(x, hpack.DecoderError) for x in want) > 50
+    for i, (gg, ww) in enumerate(zip(got, want)):
+        assert gg == ww, (i, pairs[i][1].hex())
