@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostics for the decode kernel (not part of the product): time one kernel variant
-(HPK_DEBUG_MODE env) on the config-2 batch and, in mode 3, dump per-wave timestamps."""
+(HPK_DEBUG_MODE env) on the config-2 batch (DIAG_CONFIG=config3 for the mixed one) and, in mode 3, dump per-wave timestamps."""
 import ctypes
 import json
 import os
@@ -15,7 +15,7 @@ from loona_amd.batch import decode_offsets_torch  # noqa: E402
 
 mode = int(os.environ.get("HPK_DEBUG_MODE", "0"))
 n = int(os.environ.get("DIAG_N", "1000000"))
-w = synth.config2(n=n)
+w = getattr(synth, os.environ.get("DIAG_CONFIG", "config2"))(n=n)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
     codec = HuffmanCodec(0, stream=s)
@@ -36,7 +36,7 @@ with torch.cuda.stream(s):
     e1.record(s)
     s.synchronize()
     us = e0.elapsed_time(e1) / K * 1e3
-res = {"mode": mode, "us_per_launch": round(us, 2)}
+res = {"config": w.name, "mode": mode, "us_per_launch": round(us, 2)}
 if mode in (0, 2, 3, 4):
     ok = bool((st.cpu().numpy() == 0).all()) and np.array_equal(ol.cpu().numpy(), np.diff(w.dec_off.astype(np.int64)))
     res["lengths_ok"] = ok
