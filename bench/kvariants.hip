@@ -211,6 +211,12 @@ int main(int argc, char** argv) {
     a.lut = d_lut2;
     a.lut2 = d_lut3;
     a.dbg = nullptr;
+    a.in_cap = eb;
+    a.out_cap = (uint32_t)ob;
+    uint32_t* d_err;
+    CK(hipMalloc(&d_err, 4));
+    CK(hipMemset(d_err, 0, 4));
+    a.err = d_err;
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int cu = prop.multiProcessorCount;
@@ -259,6 +265,14 @@ int main(int argc, char** argv) {
                                                                            cu, iters);
         run12<4, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1>("snake_pred_checked", d, ref_len, ref_st, ref_out,
                                                                          cu, 1);
+        // two 512-thread workgroups per CU (<= 80 KiB of LDS each): one workgroup's fill setup,
+        // barrier wait and write-back overlap the other's decode
+        run12<0, 2, 2, false, 8, 18432, 32096, 1024, 1, 2, 1>("wg2_w18", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 8, 16384, 34144, 1024, 1, 2, 1>("wg2_w16", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 8, 14336, 29696, 1024, 1, 2, 1>("wg2_w14", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<4, 2, 2, false, 8, 18432, 32096, 1024, 1, 2, 1>("wg2_w18_checked", d, ref_len, ref_st, ref_out, cu, 1);
+        // three 256-thread workgroups per CU
+        run12<0, 2, 2, false, 4, 10240, 17408, 512, 1, 3, 1>("wg3_w10", d, ref_len, ref_st, ref_out, cu, iters);
         if (!strcmp(g_only, "stamps")) {
             stamps12<2, 2, false, 16, 40960, 79104, 2048, 1>("coop1_snake", d, cu);
             stamps12<2, 2, false, 16, 40960, 79104, 2048, 1, 1, 0, 1, 0, 512, 0>("snake_nolead", d, cu);

@@ -40,7 +40,10 @@ typedef enum hpk_status {
     HPK_PADDING_TOO_LARGE = 1,  /* HuffmanDecoderError::PaddingTooLarge  (>7 residual bits) */
     HPK_INVALID_PADDING = 2,    /* HuffmanDecoderError::InvalidPadding   (residual != EOS MSBs) */
     HPK_EOS_IN_STRING = 3,      /* HuffmanDecoderError::EOSInString      (30-bit EOS decoded) */
-    HPK_OUTPUT_OVERFLOW = 4     /* not a reference error: caller's out capacity < decoded size */
+    HPK_OUTPUT_OVERFLOW = 4,    /* not a reference error: caller's out capacity < decoded size */
+    HPK_BAD_OFFSETS = 5         /* not a reference error: device-pointer call whose offsets are not
+                                   non-decreasing or pass a blob's capacity; the call's results are
+                                   void (see hpk_decode_batch) */
 } hpk_status;
 
 /* ---- API return codes (negative = the call itself failed) -------------- */
@@ -70,7 +73,8 @@ size_t hpk_huffman_encoded_len(const uint8_t* in, size_t n);
 int hpk_huffman_decode_one(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 
 /* Encode n bytes (MSB-first codes, padded with the most significant bits of
- * EOS). Returns HPK_E_OK or HPK_E_NOSPACE. */
+ * EOS). Returns HPK_E_OK or HPK_E_NOSPACE (then *out_len = cap and out holds the encoding's
+ * first cap bytes, as the batch calls' HPK_OUTPUT_OVERFLOW). */
 int hpk_huffman_encode_one(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 
 /* ---- device context ----------------------------------------------------- */
@@ -91,20 +95,39 @@ const char* hpk_last_error(const hpk_ctx* ctx); /* thread-local text of the last
  * out_blob[out_off[i] .. out_off[i+1]) (its capacity; hpk_decoded_bound of
  * its length always suffices). On return out_len[i] = bytes decoded and
  * status[i] = hpk_status. Bytes of a literal's region past out_len[i] are
- * unspecified. Offsets are u32 (one shard < 4 GiB); in_off/out_off have n+1
- * entries and must be non-decreasing. */
-int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
-                     uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len,
+ * unspecified. Offsets are u32 (one shard): in_off/out_off have n+1 entries,
+ * must be non-decreasing and at most HPK_MAX_OFFSET; in_cap / out_cap are the
+ * byte sizes of in_blob / out_blob (the reference checks a literal's length
+ * against its buffer before any Huffman work, decoder.rs:138-142).
+ *
+ * Host pointers: offsets and capacities are checked before anything is copied
+ * (HPK_E_INVAL). Device pointers: the offsets live in device memory, so the
+ * kernels check them as they read them: a literal whose offsets decrease or
+ * pass a capacity makes the kernel write HPK_BAD_OFFSETS (out_len 0) for it and
+ * for any other literals of the same batch it has not written yet, and nothing
+ * is read or written outside [in_blob, in_blob + in_cap) and
+ * [out_blob, out_blob + out_cap). The context keeps a sticky error flag: a
+ * synchronous call returns HPK_E_INVAL when it is set (and clears it);
+ * hpk_ctx_check() does the same after HPK_ASYNC calls. out_len and status
+ * must have room for n entries. */
+#define HPK_MAX_OFFSET 0xFFFFFFDFu /* offsets + a 16-byte misalignment + a 16-byte chunk stay < 2^32 */
+int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
+                     uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                      uint8_t* status, int flags);
 
 /* ---- batch encode --------------------------------------------------------
  * Symmetric: literal i = in_blob[in_off[i] .. in_off[i+1]) is Huffman-encoded
  * into out_blob[out_off[i] ..) with capacity out_off[i+1]-out_off[i]
  * (hpk_encoded_bound suffices). out_len[i] = encoded bytes; status[i] is
- * HPK_OK or HPK_OUTPUT_OVERFLOW. */
-int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
-                     uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len,
+ * HPK_OK or HPK_OUTPUT_OVERFLOW (out_len = the capacity, holding the
+ * encoding's prefix). Offsets and capacities as hpk_decode_batch. */
+int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
+                     uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                      uint8_t* status, int flags);
+
+/* Read and clear the context's sticky device error flag (after HPK_ASYNC calls; synchronises the
+ * ctx stream). Returns HPK_E_OK, HPK_E_INVAL (some call saw bad offsets) or HPK_E_DEVICE. */
+int hpk_ctx_check(hpk_ctx* ctx);
 
 /* ---- batch calls on the host CPU ----------------------------------------
  * Same layout and results as the device calls, run by `nthreads` host threads over contiguous

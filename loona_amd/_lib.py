@@ -20,6 +20,7 @@ HPK_PADDING_TOO_LARGE = 1
 HPK_INVALID_PADDING = 2
 HPK_EOS_IN_STRING = 3
 HPK_OUTPUT_OVERFLOW = 4
+HPK_BAD_OFFSETS = 5  # device-pointer call with decreasing offsets / offsets past a capacity
 
 HPK_E_OK = 0
 HPK_E_INVAL = -1
@@ -30,6 +31,7 @@ HPK_E_NODEVICE = -4
 HPK_PTR_HOST = 0x0
 HPK_PTR_DEVICE = 0x1
 HPK_ASYNC = 0x2
+HPK_MAX_OFFSET = 0xFFFFFFDF  # offsets of one shard stay at or below this (hpk.h)
 
 # every symbol include/hpk.h declares (tests/test_host.py checks the .so exports all of them)
 EXPORTS = (
@@ -43,6 +45,7 @@ EXPORTS = (
     "hpk_ctx_set_stream",
     "hpk_ctx_stream",
     "hpk_ctx_sync",
+    "hpk_ctx_check",
     "hpk_last_error",
     "hpk_decode_batch",
     "hpk_encode_batch",
@@ -121,11 +124,14 @@ def lib() -> ctypes.CDLL:
         L.hpk_ctx_stream.restype = ctypes.c_void_p
         L.hpk_ctx_sync.argtypes = [ctypes.c_void_p]
         L.hpk_ctx_sync.restype = ctypes.c_int
+        L.hpk_ctx_check.argtypes = [ctypes.c_void_p]
+        L.hpk_ctx_check.restype = ctypes.c_int
         L.hpk_last_error.argtypes = [ctypes.c_void_p]
         L.hpk_last_error.restype = ctypes.c_char_p
         for fn in (L.hpk_decode_batch, L.hpk_encode_batch):
-            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
-                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32,
+                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_int]
             fn.restype = ctypes.c_int
         for fn in (L.hpk_decode_batch_cpu, L.hpk_encode_batch_cpu):
             fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,

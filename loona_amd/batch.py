@@ -4,9 +4,13 @@ Layout (one shard, u32 offsets): literal i is in_blob[in_off[i]:in_off[i+1]]; it
 out_blob[out_off[i]:out_off[i+1]] (capacity), out_len[i] bytes are valid, status[i] is the
 hpk_status (0 ok, 1 PaddingTooLarge, 2 InvalidPadding, 3 EOSInString, 4 output overflow).
 
-Device tensors go straight to the kernels on the context's stream (by default torch's current
-stream, so torch events and the kernels share one timeline). Host numpy arrays go through the
-library's own H2D/D2H staging. There is no CPU fallback anywhere in this module.
+Device tensors go straight to the kernels on the codec's stream: by default torch's current
+stream on the codec's device at the time of each call, so torch ops that produced the inputs and
+the caching allocator's reuse of the outputs are ordered with the kernels. Host numpy arrays go
+through the library's own H2D/D2H staging. Every buffer is checked before it reaches the C ABI
+(dtype, contiguity, device, room for n entries), and the C ABI gets each blob's capacity, so
+offsets past a blob are rejected on the device (status HPK_BAD_OFFSETS) instead of read or written.
+There is no CPU fallback anywhere in this module.
 """
 
 from __future__ import annotations
@@ -68,19 +72,52 @@ def encode_offsets_np(in_off):
     return out.astype(U32)
 
 
-def _ptr(x):
-    if x is None:
-        return None
-    if isinstance(x, np.ndarray):
-        return x.ctypes.data_as(ctypes.c_void_p)
-    return ctypes.c_void_p(x.data_ptr())  # torch tensor
+_OFF_DTYPES = ("int32", "uint32")
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _arg(x, name, kinds, min_len, device_index=None):
+    """(pointer, byte size) of a contiguous numpy array or torch tensor, after checking its dtype
+    (one of `kinds`), its length (>= min_len entries) and, for device calls, that it is a CUDA
+    tensor on the codec's device. Raises ValueError / TypeError instead of handing the C ABI a
+    buffer it would misread (an int64 offset tensor read as u32 halves, a view, a short array)."""
+    if _is_torch(x):
+        dt = str(x.dtype).replace("torch.", "")
+        if device_index is not None:
+            if not x.is_cuda or x.device.index != device_index:
+                raise ValueError(f"{name}: expected a tensor on cuda:{device_index}, got {x.device}")
+        elif x.is_cuda:
+            raise ValueError(f"{name}: host-pointer call given a CUDA tensor")
+        if not x.is_contiguous():
+            raise ValueError(f"{name}: tensor must be contiguous")
+        n, nbytes, ptr = x.numel(), x.numel() * x.element_size(), x.data_ptr()
+    elif isinstance(x, np.ndarray):
+        if device_index is not None:
+            raise ValueError(f"{name}: device call given a host numpy array")
+        dt = str(x.dtype)
+        if not x.flags["C_CONTIGUOUS"]:
+            raise ValueError(f"{name}: array must be C-contiguous")
+        n, nbytes, ptr = x.size, x.nbytes, x.ctypes.data
+    else:
+        raise TypeError(f"{name}: expected a numpy array or torch tensor, got {type(x).__name__}")
+    if dt not in kinds:
+        raise TypeError(f"{name}: dtype {dt} not in {kinds}")
+    if n < min_len:
+        raise ValueError(f"{name}: {n} entries, need >= {min_len}")
+    return ctypes.c_void_p(ptr), nbytes
 
 
 class HuffmanCodec:
     """One device context (hpk_ctx): a HIP stream + LDS-staged decode tables on one GPU.
 
     loona is thread-per-core and !Send (crates/buffet/src/lib.rs:38-49): use one codec per
-    host thread."""
+    host thread.
+
+    stream: None (default) = torch's current stream on `device` at each call; a torch.cuda.Stream
+    or raw hipStream_t int = that stream; "own" = the context's own non-blocking stream."""
 
     def __init__(self, device: int = 0, stream=None):
         self._L = _lib.lib()
@@ -89,7 +126,9 @@ class HuffmanCodec:
         if not h:
             raise RuntimeError(f"hpk_ctx_create({device}) failed: {_lib.last_error()}")
         self._h = h
-        if stream is not None:
+        self._follow_torch = stream is None
+        self._bound = None
+        if stream is not None and stream != "own":
             self.set_stream(stream)
 
     def close(self):
@@ -111,34 +150,70 @@ class HuffmanCodec:
 
     def set_stream(self, stream):
         """stream: a torch.cuda.Stream (its handle 0 = the legacy null stream), a raw hipStream_t
-        int, or None (the ctx's own non-blocking stream)."""
+        int, or None (the ctx's own non-blocking stream). Fixes the stream for later calls."""
+        self._follow_torch = False
+        self._bind(stream)
+
+    def _bind(self, stream):
         if stream is None:
             arg = None
         else:
             raw = int(getattr(stream, "cuda_stream", stream))
             arg = ctypes.c_void_p(raw) if raw else ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF)  # HPK_STREAM_LEGACY
         _lib.check(self._L.hpk_ctx_set_stream(self._h, arg), "hpk_ctx_set_stream")
+        self._bound = None if arg is None else arg.value
+
+    def _follow(self):
+        """Bind torch's current stream on the codec's device (default mode)."""
+        if not self._follow_torch:
+            return
+        import torch
+
+        s = torch.cuda.current_stream(self.device)
+        raw = int(s.cuda_stream) or (-1 & 0xFFFFFFFFFFFFFFFF)
+        if raw != self._bound:
+            self._bind(s)
 
     def sync(self):
         _lib.check(self._L.hpk_ctx_sync(self._h), "hpk_ctx_sync")
 
+    def check(self):
+        """Sticky device error flag (bad offsets in an earlier HPK_ASYNC call): raises if set."""
+        _lib.check(self._L.hpk_ctx_check(self._h), "hpk_ctx_check")
+
     # -- raw entry points --------------------------------------------------------------------
-    def _call(self, fn, name, in_blob, in_off, n, out_blob, out_off, out_len, status, flags):
-        rc = fn(self._h, _ptr(in_blob), _ptr(in_off), ctypes.c_uint32(n), _ptr(out_blob), _ptr(out_off),
-                _ptr(out_len), _ptr(status), flags)
+    def _call(self, fn, name, in_blob, in_off, out_blob, out_off, out_len, status, device, sync):
+        dev = self.device if device else None
+        n = (int(in_off.shape[0]) if hasattr(in_off, "shape") else len(in_off)) - 1
+        if n < 0:
+            raise ValueError("in_off needs n+1 >= 1 entries")
+        if n >= 2**32:
+            raise ValueError("a batch holds at most 2^32 - 1 literals")
+        pi, in_cap = _arg(in_blob, "in_blob", ("uint8",), 0, dev)
+        pio, _ = _arg(in_off, "in_off", _OFF_DTYPES, n + 1, dev)
+        po, out_cap = _arg(out_blob, "out_blob", ("uint8",), 0, dev)
+        poo, _ = _arg(out_off, "out_off", _OFF_DTYPES, n + 1, dev)
+        pl, _ = _arg(out_len, "out_len", ("int32", "uint32"), n, dev)
+        ps, _ = _arg(status, "status", ("uint8",), n, dev)
+        if device:
+            self._follow()
+            flags = _lib.HPK_PTR_DEVICE | (0 if sync else _lib.HPK_ASYNC)
+        else:
+            flags = _lib.HPK_PTR_HOST
+        rc = fn(self._h, pi, in_cap, pio, ctypes.c_uint32(n), po, out_cap, poo, pl, ps, flags)
         _lib.check(rc, name)
 
     def decode_into(self, in_blob, in_off, out_blob, out_off, out_len, status, device=True, sync=False):
-        n = int(in_off.shape[0]) - 1
-        flags = _lib.HPK_PTR_DEVICE | (0 if sync else _lib.HPK_ASYNC) if device else _lib.HPK_PTR_HOST
-        self._call(self._L.hpk_decode_batch, "hpk_decode_batch", in_blob, in_off, n, out_blob, out_off, out_len,
-                   status, flags)
+        """hpk_decode_batch. device=True: CUDA tensors on the codec's device, enqueued (sync=False:
+        HPK_ASYNC; bad offsets then show as status HPK_BAD_OFFSETS and in check()). device=False:
+        host numpy arrays, staged and synchronous."""
+        self._call(self._L.hpk_decode_batch, "hpk_decode_batch", in_blob, in_off, out_blob, out_off, out_len,
+                   status, device, sync)
 
     def encode_into(self, in_blob, in_off, out_blob, out_off, out_len, status, device=True, sync=False):
-        n = int(in_off.shape[0]) - 1
-        flags = _lib.HPK_PTR_DEVICE | (0 if sync else _lib.HPK_ASYNC) if device else _lib.HPK_PTR_HOST
-        self._call(self._L.hpk_encode_batch, "hpk_encode_batch", in_blob, in_off, n, out_blob, out_off, out_len,
-                   status, flags)
+        """hpk_encode_batch, same conventions as decode_into."""
+        self._call(self._L.hpk_encode_batch, "hpk_encode_batch", in_blob, in_off, out_blob, out_off, out_len,
+                   status, device, sync)
 
     # -- host (numpy) convenience ------------------------------------------------------------
     def decode_host(self, in_blob, in_off, out_off=None):

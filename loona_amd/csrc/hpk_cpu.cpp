@@ -111,17 +111,24 @@ int hpk_cpu_encode(const hpk_tables* t, const uint8_t* in, size_t n, uint8_t* ou
     uint64_t acc = 0;
     int nb = 0;
     size_t o = 0;
+    // on HPK_E_NOSPACE *out_len = cap: out holds the encoding's first cap bytes (as the device kernels)
     for (size_t i = 0; i < n; ++i) {
         acc = (acc << t->len[in[i]]) | t->code[in[i]];
         nb += t->len[in[i]];
         while (nb >= 8) {
-            if (o >= cap) return HPK_E_NOSPACE;
+            if (o >= cap) {
+                *out_len = o;
+                return HPK_E_NOSPACE;
+            }
             nb -= 8;
             out[o++] = (uint8_t)(acc >> nb);
         }
     }
     if (nb) {
-        if (o >= cap) return HPK_E_NOSPACE;
+        if (o >= cap) {
+            *out_len = o;
+            return HPK_E_NOSPACE;
+        }
         out[o++] = (uint8_t)((acc << (8 - nb)) | (0xFFu >> nb));
     }
     *out_len = o;

@@ -66,6 +66,10 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     }
     if ((e = hipMemcpy(c->d_lo, t->lo, sizeof(t->lo), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload lo", e);
     if ((e = hipMemcpy(c->d_codes, packed, sizeof(packed), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload codes", e);
+    if ((e = hipHostMalloc((void**)&c->h_err, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+        return fail("hipHostMalloc err flag", e);
+    *c->h_err = 0;
+    if ((e = hipHostGetDevicePointer((void**)&c->d_err, c->h_err, 0)) != hipSuccess) return fail("err flag pointer", e);
     return c;
 }
 
@@ -82,6 +86,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
+    if (c->h_err) (void)hipHostFree(c->h_err);
     for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
         if (c->ev_in[j]) (void)hipEventDestroy(c->ev_in[j]);
         if (c->ev_run[j]) (void)hipEventDestroy(c->ev_run[j]);
@@ -132,29 +137,49 @@ static int grow(void** p, size_t* cap, size_t need) {
     return HPK_E_OK;
 }
 
-static int check_offsets(const uint32_t* off, uint32_t n) {
+static int check_offsets(const uint32_t* off, uint32_t n, size_t cap) {
     for (uint32_t i = 0; i < n; ++i)
         if (off[i + 1] < off[i]) return hpk_set_err_msg("offsets must be non-decreasing", HPK_E_INVAL);
+    if (off[n] > cap || off[n] > HPK_MAX_OFFSET) return hpk_set_err_msg("offsets pass the blob's capacity", HPK_E_INVAL);
     return HPK_E_OK;
 }
 
-typedef int (*launch_fn)(hpk_ctx*, const uint8_t*, const uint32_t*, uint32_t, uint8_t*, const uint32_t*,
-                         uint32_t*, uint8_t*);
+// read and clear the sticky device error flag (the ctx stream must be synchronised)
+static int take_err(hpk_ctx* c) {
+    if (!__atomic_exchange_n(c->h_err, 0u, __ATOMIC_ACQ_REL)) return HPK_E_OK;
+    return hpk_set_err_msg("a batch had non-monotone offsets or offsets past a blob's capacity (HPK_BAD_OFFSETS)",
+                           HPK_E_INVAL);
+}
 
-static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
-                     uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int flags) {
+extern "C" int hpk_ctx_check(hpk_ctx* c) {
+    if (!c) return HPK_E_INVAL;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return take_err(c);
+}
+
+typedef int (*launch_fn)(hpk_ctx*, const hpk_batch&);
+
+static uint32_t clamp_cap(size_t cap) { return cap > HPK_MAX_OFFSET ? HPK_MAX_OFFSET : (uint32_t)cap; }
+
+static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
+                     uint32_t n, uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
+                     uint8_t* status, int flags) {
     if (!c || !in_off || !out_off || (n && (!out_len || !status))) return hpk_set_err_msg("null argument", HPK_E_INVAL);
     HIP_TRY(hipSetDevice(c->device));
     if (flags & HPK_PTR_DEVICE) {
         if (n == 0) return HPK_E_OK;
         if (!in_blob || !out_blob) return hpk_set_err_msg("null blob", HPK_E_INVAL);
-        int rc = fn(c, in_blob, in_off, n, out_blob, out_off, out_len, status);
+        const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), out_off, out_len, status};
+        int rc = fn(c, b);
         if (rc) return rc;
-        if (!(flags & HPK_ASYNC)) HIP_TRY(hipStreamSynchronize(c->stream));
+        if (!(flags & HPK_ASYNC)) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            return take_err(c);
+        }
         return HPK_E_OK;
     }
     // host pointers: validate, stage, run, copy back
-    if (check_offsets(in_off, n) || check_offsets(out_off, n)) return HPK_E_INVAL;
+    if (check_offsets(in_off, n, in_cap) || check_offsets(out_off, n, out_cap)) return HPK_E_INVAL;
     if (n == 0) return HPK_E_OK;
     const size_t in_bytes = in_off[n], out_bytes = out_off[n];
     if ((in_bytes && !in_blob) || (out_bytes && !out_blob)) return hpk_set_err_msg("null blob", HPK_E_INVAL);
@@ -206,7 +231,9 @@ static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uin
         HIP_TRY(hipMemcpyAsync(d_out_off + a, out_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
         HIP_TRY(hipEventRecord(c->ev_in[j], c->h2d));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_in[j], 0));
-        if ((rc = fn(c, c->d_in, d_in_off + a, b - a, c->d_out, d_out_off + a, d_len + a, c->d_st + a))) return rc;
+        const hpk_batch bt{c->d_in, (uint32_t)in_bytes, d_in_off + a, b - a, c->d_out, (uint32_t)out_bytes,
+                           d_out_off + a, d_len + a, c->d_st + a};
+        if ((rc = fn(c, bt))) return rc;
         HIP_TRY(hipEventRecord(c->ev_run[j], c->stream));
         HIP_TRY(hipStreamWaitEvent(c->d2h, c->ev_run[j], 0));
         if (oe > ob) HIP_TRY(hipMemcpyAsync(out_blob + ob, c->d_out + ob, oe - ob, hipMemcpyDeviceToHost, c->d2h));
@@ -214,17 +241,19 @@ static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uin
         HIP_TRY(hipMemcpyAsync(status + a, c->d_st + a, b - a, hipMemcpyDeviceToHost, c->d2h));
     }
     HIP_TRY(hipStreamSynchronize(c->d2h));
-    return HPK_E_OK;
+    return take_err(c);
 }
 
-extern "C" int hpk_decode_batch(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
-                                uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len, uint8_t* status,
-                                int flags) {
-    return run_batch(hpk_launch_decode, c, in_blob, in_off, n, out_blob, out_off, out_len, status, flags);
+extern "C" int hpk_decode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
+                                uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
+                                uint8_t* status, int flags) {
+    return run_batch(hpk_launch_decode, c, in_blob, in_cap, in_off, n, out_blob, out_cap, out_off, out_len, status,
+                     flags);
 }
 
-extern "C" int hpk_encode_batch(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
-                                uint8_t* out_blob, const uint32_t* out_off, uint32_t* out_len, uint8_t* status,
-                                int flags) {
-    return run_batch(hpk_launch_encode, c, in_blob, in_off, n, out_blob, out_off, out_len, status, flags);
+extern "C" int hpk_encode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
+                                uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
+                                uint8_t* status, int flags) {
+    return run_batch(hpk_launch_encode, c, in_blob, in_cap, in_off, n, out_blob, out_cap, out_off, out_len, status,
+                     flags);
 }

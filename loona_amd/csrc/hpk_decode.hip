@@ -58,17 +58,11 @@ constexpr int kDefer = HPK_DEFER;  // the previous fill's write-back issued duri
 constexpr int kPredSt = HPK_PREDST;  // unconditional byte stores in the lane step (dummy slots)
 #define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt>
 
+#ifdef HPK_DIAG
+// Diagnostic build (libhpk_diag.so, `make diag`; never the product library): HPK_DEBUG_MODE selects
+// 1 no decode, 2 no output stores, 3 per-wave stamps (16 x u64 per wave, hpk_debug_stamps),
+// 4 every store bounds-checked (hpk_debug_check).
 static int g_debug_mode = -1;
-
-int hpk_decode_setup() {
-    if (g_debug_mode < 0) {
-        const char* dm = getenv("HPK_DEBUG_MODE");
-        g_debug_mode = dm ? atoi(dm) : 0;
-    }
-    return HPK_E_OK;  // the decode kernel's LDS is static: no attribute to set
-}
-
-// diagnostic stamps buffer (HPK_DEBUG_MODE=3): 16 x u64 per wave
 static unsigned long long* g_dbg = nullptr;
 static size_t g_dbg_n = 0;
 
@@ -82,33 +76,39 @@ extern "C" int hpk_debug_stamps(unsigned long long* host, size_t cap_entries) {
     if (hipMemcpy(host, g_dbg, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     return (int)n;
 }
+#endif
 
-int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
-                      const uint32_t* out_off, uint32_t* out_len, uint8_t* status) {
-    int rc = hpk_decode_setup();
-    if (rc) return rc;
+int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     DecodeArgs a;
-    const uintptr_t ip = (uintptr_t)in_blob;
+    const uintptr_t ip = (uintptr_t)b.in_blob;
     a.in_base = (const uint8_t*)(ip & ~(uintptr_t)15);
     a.in_mis = (uint32_t)(ip & 15);
-    a.in_off = in_off;
-    a.n = n;
-    const uintptr_t op = (uintptr_t)out_blob;
+    a.in_off = b.in_off;
+    a.n = b.n;
+    const uintptr_t op = (uintptr_t)b.out_blob;
     a.out_base = (uint8_t*)(op & ~(uintptr_t)15);
     a.out_mis = (uint32_t)(op & 15);
-    a.out_off = out_off;
-    a.out_len = out_len;
-    a.status = status;
+    a.out_off = b.out_off;
+    a.out_len = b.out_len;
+    a.status = b.status;
     a.t8 = c->d_t8;
     a.lo = c->d_lo;
     a.lut = c->d_lut;
     a.lut2 = c->d_lut2;
     a.dbg = nullptr;
+    a.in_cap = b.in_cap;
+    a.out_cap = b.out_cap;
+    a.err = c->d_err;
     // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
-    uint64_t blocks = ((uint64_t)n + 63) / 64;
+    uint64_t blocks = ((uint64_t)b.n + 63) / 64;
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
+#ifdef HPK_DIAG
+    if (g_debug_mode < 0) {
+        const char* dm = getenv("HPK_DEBUG_MODE");
+        g_debug_mode = dm ? atoi(dm) : 0;
+    }
     switch (g_debug_mode) {
         case 1:
             hipLaunchKernelGGL(DEC_KERNEL(1), grid, block, 0, c->stream, a);
@@ -133,6 +133,9 @@ int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off
         default:
             hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
     }
+#else
+    hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
+#endif
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
 }

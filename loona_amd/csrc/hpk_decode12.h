@@ -586,17 +586,19 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     const uint32_t lane = tid & 63u;
     const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
-    const uint32_t in_end = a.in_off[a.n] + a.in_mis;
+    // offsets are clamped to the input capacity wherever they bound a read, so bad offsets (caught
+    // per fill below) never move a window past the blob
+    const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
     // last chunk holding a byte of THIS workgroup's literals: windows never read past it
-    const uint32_t r_end = a.in_off[BB] + a.in_mis;
+    const uint32_t r_end = min(min(a.in_off[BB], a.in_cap) + a.in_mis, in_end);
     const uint32_t rlast16 = r_end ? (r_end - 1) >> 4 : 0;
     // kEven: the range is cut into the fewest fills the window allows, of about equal input size
     // (a greedy cut leaves a small last fill that still costs a whole fill's setup, slowest literal
     // and write-back); the effective window is that size plus a margin for literal granularity
     uint32_t kWe = (uint32_t)kW;
     if (kEven) {
-        const uint32_t R = r_end - ((a.in_off[BA] + a.in_mis) & ~15u);
+        const uint32_t R = r_end - min((min(a.in_off[BA], a.in_cap) + a.in_mis) & ~15u, r_end);
         const uint32_t nf = (R + (uint32_t)kW - 1u) / (uint32_t)kW;
         if (nf > 1u) kWe = min((uint32_t)kW, (R + nf - 1u) / nf + 512u);
     }
@@ -732,17 +734,21 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             s_ctr[2] = gin;
             s_ctr[3] = gout;
             s_ctr[4] = 0;
+            s_ctr[5] = 0;
         }
         lds_barrier();
         uint32_t ex[R], ey[R], pos[R];
         uint32_t kw = 0;
+        bool bad = false;  // a literal of this fill's range with decreasing offsets or offsets past a capacity
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            bad |= t < cntl && !(P.io0[r] <= P.io1[r] && P.io1[r] <= a.in_cap && P.oo0[r] <= P.oo1[r] &&
+                                 P.oo1[r] <= a.out_cap);
             const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
             const uint32_t o0 = P.oo0[r] + a.out_mis, o1 = P.oo1[r] + a.out_mis;
             // fitting literals form a prefix (offsets are non-decreasing)
-            const bool fits = t < cntl && p1 - base16 <= kWe && o1 - ob16 <= (uint32_t)kImg;
+            const bool fits = !bad && t < cntl && p1 - base16 <= kWe && o1 - ob16 <= (uint32_t)kImg;
             pos[r] = 0xFFFFFFFFu;
             if (fits) {
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
@@ -767,12 +773,22 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
         if (lane == 0 && kw) atomicAdd(&s_ctr[0], kw);
+        if (__any(bad) && lane == 0) s_ctr[5] = 1u;
         lds_barrier();
         if (kMode == 3) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             t_setA += t1 - tb0;  // (mode 3: offsets in, entries made)
             if (cur == BA) t_A0 = t1 - tb0;
             tb0 = t1;
+        }
+        if (s_ctr[5]) {  // bad offsets (block-uniform): the range's remaining literals are void, nothing
+                         // more is decoded or written here (the previous, valid fill is flushed below)
+            for (uint32_t i = cur + tid; i < BB; i += G::kBlock) {
+                a.out_len[i] = 0;
+                a.status[i] = (uint8_t)HPK_BAD_OFFSETS;
+            }
+            if (tid == 0) *a.err = 1u;
+            break;
         }
         const uint32_t k = s_ctr[0];
         if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global

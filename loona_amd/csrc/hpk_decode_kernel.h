@@ -30,6 +30,8 @@ struct DecodeArgs {
     const uint32_t* lut;  // two-symbol table (hpk_code.h), step 8
     const uint32_t* lut2; // the same in the LUT2 layout (decode v12)
     unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
+    uint32_t in_cap, out_cap;  // blob sizes (clamped to HPK_MAX_OFFSET): larger offsets are bad
+    uint32_t* err;             // sticky error flag (host-mapped): set to 1 on bad offsets
 };
 
 // Per-lane state of the literal being decoded.

@@ -34,6 +34,23 @@ struct hpk_ctx {
     hipStream_t d2h = nullptr;
     hipEvent_t ev_in[kMaxChunks] = {};
     hipEvent_t ev_run[kMaxChunks] = {};
+    // sticky error flag: host-mapped, written (plain store of 1) by a kernel that saw bad offsets
+    uint32_t* h_err = nullptr;
+    uint32_t* d_err = nullptr;
+};
+
+// One batch call as the launchers see it: capacities clamped to HPK_MAX_OFFSET (offsets above
+// them are bad whatever the buffer size).
+struct hpk_batch {
+    const uint8_t* in_blob;
+    uint32_t in_cap;
+    const uint32_t* in_off;
+    uint32_t n;
+    uint8_t* out_blob;
+    uint32_t out_cap;
+    const uint32_t* out_off;
+    uint32_t* out_len;
+    uint8_t* status;
 };
 
 int hpk_set_err(const char* what, hipError_t e);
@@ -45,12 +62,7 @@ int hpk_set_err_msg(const char* what, int code);
         if (_e != hipSuccess) return hpk_set_err(#call, _e);     \
     } while (0)
 
-// one-time per-process kernel attribute setup (dynamic LDS above 64 KiB)
-int hpk_decode_setup();
-
-int hpk_launch_decode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
-                      const uint32_t* out_off, uint32_t* out_len, uint8_t* status);
-int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
-                      const uint32_t* out_off, uint32_t* out_len, uint8_t* status);
+int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b);
+int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b);
 
 __device__ __forceinline__ uint32_t hpk_bswap32(uint32_t x) { return __builtin_bswap32(x); }

@@ -33,6 +33,8 @@ struct EncodeArgs {
     uint32_t in_mis;
     uint8_t* out_base;
     uint32_t out_mis;
+    uint32_t in_cap, out_cap;  // blob sizes (clamped to HPK_MAX_OFFSET): larger offsets are bad
+    uint32_t* err;             // sticky error flag (host-mapped): set to 1 on bad offsets
 };
 
 // One literal, one lane, global memory: v1's loop (also the large-literal path of v2).
@@ -71,6 +73,7 @@ __device__ __forceinline__ void encode_serial(const EncodeArgs& a, const uint32_
 
 #define ENC_BLOCK 256
 
+#ifdef HPK_DIAG
 __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
     __shared__ uint32_t s_code[256];
     __shared__ uint8_t s_len[256];
@@ -82,6 +85,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
     for (uint32_t i = blockIdx.x * ENC_BLOCK + threadIdx.x; i < a.n; i += gridDim.x * ENC_BLOCK)
         encode_serial(a, s_code, s_len, i);
 }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // v2
@@ -101,7 +105,7 @@ struct EncLds {
     uint32_t code1[256];         // serial path: codes
     uint8_t len1[256];           // serial path: lengths
     uint32_t wf[16], wv[16];     // per-wave scan totals
-    uint32_t ctr[4];             // [0] literals in the tile
+    uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen
 };
 
 
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     }
     const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
-    const uint32_t in_end = a.in_off[a.n] + a.in_mis;
+    const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;  // (clamped: reads stay in the blob)
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
     const uint4* g_in = reinterpret_cast<const uint4*>(a.in_base);
     // the next tile's input chunks and offsets are loaded into registers while the current one is
@@ -167,7 +171,10 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         const uint32_t cntl = min((uint32_t)kEQ, BB - cur);
         const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
         lds_barrier_e();  // the previous tile's image is out
-        if (tid == 0) S.ctr[0] = 0;
+        if (tid == 0) {
+            S.ctr[0] = 0;
+            S.ctr[1] = 0;
+        }
         {  // clear the image
             uint4* i16 = reinterpret_cast<uint4*>(S.img);
             for (uint32_t c = tid; c < (uint32_t)kEO / 16; c += kEB) i16[c] = make_uint4(0, 0, 0, 0);
@@ -175,13 +182,19 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         lds_barrier_e();
         // which literals fit (a prefix: offsets are non-decreasing)
         uint32_t kw = 0;
+        bool bad = false;  // a literal of the tile's range with decreasing offsets or offsets past a capacity
+#pragma unroll
+        for (int r = 0; r < kEMeta; ++r) {
+            const uint32_t t = tid + (uint32_t)kEB * r;
+            bad |= t < cntl && !(pi0[r] <= pi1[r] && pi1[r] <= a.in_cap && po0[r] <= po1[r] && po1[r] <= a.out_cap);
+        }
 #pragma unroll
         for (int r = 0; r < kEMeta; ++r) {
             const uint32_t t = tid + (uint32_t)kEB * r;
             bool fits = false;
             const uint32_t i0 = pi0[r] + a.in_mis, i1 = pi1[r] + a.in_mis;
             const uint32_t o0 = po0[r] + a.out_mis, o1 = po1[r] + a.out_mis;
-            if (t < cntl) fits = i1 - base16 <= (uint32_t)kETile && o1 - ob16 <= (uint32_t)kEO;
+            if (t < cntl && !bad) fits = i1 - base16 <= (uint32_t)kETile && o1 - ob16 <= (uint32_t)kEO;
             if (fits) {
                 S.ioff[t] = i0 - base16;
                 S.ooff[t] = o0 - ob16;
@@ -192,8 +205,17 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             kw += (uint32_t)__popcll(__ballot(fits));
         }
         if (lane == 0 && kw) atomicAdd(&S.ctr[0], kw);
+        if (__any(bad) && lane == 0) S.ctr[1] = 1u;
         const uint4 chc0 = ch[0], chc1 = ch[1];
         lds_barrier_e();
+        if (S.ctr[1]) {  // bad offsets (block-uniform): the range's remaining literals are void
+            for (uint32_t i = cur + tid; i < BB; i += kEB) {
+                a.out_len[i] = 0;
+                a.status[i] = (uint8_t)HPK_BAD_OFFSETS;
+            }
+            if (tid == 0) *a.err = 1u;
+            break;
+        }
         const uint32_t k = S.ctr[0];
         if (k == 0) {  // literal `cur` alone exceeds a tile: one lane, global memory
             if (tid == 0) encode_serial(a, S.code1, S.len1, cur);
@@ -394,50 +416,62 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     }
 }
 
+#ifdef HPK_DIAG
 static int g_encode_v1 = -1, g_encode_cfg = 0;
+#endif
 
 }  // namespace
 
-int hpk_launch_encode(hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
-                      const uint32_t* out_off, uint32_t* out_len, uint8_t* status) {
-    if (g_encode_v1 < 0) {
-        const char* e = getenv("HPK_ENCODE_V1");
-        g_encode_v1 = e && atoi(e) ? 1 : 0;
-        const char* w = getenv("HPK_ENCODE_CFG");  // geometry variants for measurements (0 = product)
-        g_encode_cfg = w ? atoi(w) : 0;
-    }
-    EncodeArgs a{in_blob, in_off, n, out_blob, out_off, out_len, status, c->d_codes};
-    const uintptr_t ip = (uintptr_t)in_blob, op = (uintptr_t)out_blob;
+int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
+    EncodeArgs a{b.in_blob, b.in_off, b.n, b.out_blob, b.out_off, b.out_len, b.status, c->d_codes};
+    const uintptr_t ip = (uintptr_t)b.in_blob, op = (uintptr_t)b.out_blob;
     a.in_base = (const uint8_t*)(ip & ~(uintptr_t)15);
     a.in_mis = (uint32_t)(ip & 15);
     a.out_base = (uint8_t*)(op & ~(uintptr_t)15);
     a.out_mis = (uint32_t)(op & 15);
+    a.in_cap = b.in_cap;
+    a.out_cap = b.out_cap;
+    a.err = c->d_err;
+    int cfg = 0;
+#ifdef HPK_DIAG
+    // diagnostic build only: v1 (one lane per literal, no offset checks) and geometry variants
+    if (g_encode_v1 < 0) {
+        const char* e = getenv("HPK_ENCODE_V1");
+        g_encode_v1 = e && atoi(e) ? 1 : 0;
+        const char* w = getenv("HPK_ENCODE_CFG");
+        g_encode_cfg = w ? atoi(w) : 0;
+    }
+    cfg = g_encode_cfg;
     if (g_encode_v1) {
-        uint64_t blocks = ((uint64_t)n + ENC_BLOCK - 1) / ENC_BLOCK;
+        uint64_t blocks = ((uint64_t)b.n + ENC_BLOCK - 1) / ENC_BLOCK;
         const uint64_t max_blocks = (uint64_t)c->num_cu * 8;
         if (blocks > max_blocks) blocks = max_blocks;
         if (blocks < 1) blocks = 1;
         hipLaunchKernelGGL(hpk_encode_kernel, dim3((uint32_t)blocks), dim3(ENC_BLOCK), 0, c->stream, a);
-    } else {
-        // per = workgroups per CU; fewer when the batch is small (>= ~64 literals per workgroup)
-        const int per = (g_encode_cfg == 1 || g_encode_cfg == 2) ? 1 : 2;
-        uint64_t blocks = ((uint64_t)n + 63) / 64;
-        if (blocks > (uint64_t)c->num_cu * per) blocks = (uint64_t)c->num_cu * per;
-        if (blocks < 1) blocks = 1;
-        const dim3 grid((uint32_t)blocks);
-        switch (g_encode_cfg) {
-            case 1:  // one 1024-thread workgroup per CU, 32 KiB tiles
-                hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 32>), grid, dim3(1024), 0, c->stream, a);
-                break;
-            case 2:  // one 1024-thread workgroup per CU, 16 bytes per thread
-                hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 16>), grid, dim3(1024), 0, c->stream, a);
-                break;
-            case 3:  // two 512-thread workgroups per CU, 16 bytes per thread
-                hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 16>), grid, dim3(512), 0, c->stream, a);
-                break;
-            default:  // product: two 512-thread workgroups per CU, 32 bytes per thread
-                hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 32>), grid, dim3(512), 0, c->stream, a);
-        }
+        HIP_TRY(hipGetLastError());
+        return HPK_E_OK;
+    }
+#endif
+    // per = workgroups per CU; fewer when the batch is small (>= ~64 literals per workgroup)
+    const int per = (cfg == 1 || cfg == 2) ? 1 : 2;
+    uint64_t blocks = ((uint64_t)b.n + 63) / 64;
+    if (blocks > (uint64_t)c->num_cu * per) blocks = (uint64_t)c->num_cu * per;
+    if (blocks < 1) blocks = 1;
+    const dim3 grid((uint32_t)blocks);
+    switch (cfg) {
+#ifdef HPK_DIAG
+        case 1:  // one 1024-thread workgroup per CU, 32 KiB tiles
+            hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 32>), grid, dim3(1024), 0, c->stream, a);
+            break;
+        case 2:  // one 1024-thread workgroup per CU, 16 bytes per thread
+            hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 16>), grid, dim3(1024), 0, c->stream, a);
+            break;
+        case 3:  // two 512-thread workgroups per CU, 16 bytes per thread
+            hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 16>), grid, dim3(512), 0, c->stream, a);
+            break;
+#endif
+        default:  // product: two 512-thread workgroups per CU, 32 bytes per thread
+            hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 32>), grid, dim3(512), 0, c->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;

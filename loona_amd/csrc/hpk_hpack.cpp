@@ -512,8 +512,8 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
             memcpy(in.data() + in_off[lbase[t] + j], blocks + thoff[t][j], thlen[t][j]);
     });
     if (n) {
-        const int rc = ctx ? hpk_decode_batch(ctx, in.data(), in_off.data(), n, dec.data(), out_off.data(), len.data(),
-                                              st.data(), HPK_PTR_HOST)
+        const int rc = ctx ? hpk_decode_batch(ctx, in.data(), in.size(), in_off.data(), n, dec.data(), dec.size(), out_off.data(),
+                                              len.data(), st.data(), HPK_PTR_HOST)
                            : hpk_decode_batch_cpu(in.data(), in_off.data(), n, dec.data(), out_off.data(), len.data(),
                                                   st.data(), 0);
         if (rc) return rc;

@@ -10,6 +10,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the diagnostic kernel variants live only in libhpk_diag.so (`make -C loona_amd/csrc diag`)
+os.environ.setdefault("HPK_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                              "loona_amd", "libhpk_diag.so"))
 from loona_amd import HuffmanCodec, _lib, synth  # noqa: E402
 from loona_amd.batch import decode_offsets_torch  # noqa: E402
 

@@ -179,3 +179,71 @@ def test_tables_lut_and_lo_decode_every_code():
         data = bytes([s]) + follow
         assert d.decode(hpack_ref.huffman_encode(data)) == data
     assert len(ref) == 257
+
+
+def test_cpu_encode_overflow_matches_device_contract():
+    """hpk_encode_batch_cpu on an undersized capacity: HPK_OUTPUT_OVERFLOW with out_len = capacity
+    and the encoding's prefix, as the device kernels (tests/test_gpu.py
+    test_encode_small_capacity_and_huge_literal); the scalar call reports the same length."""
+    L = _lib.lib()
+    s = b"www.example.com"
+    want = oracle_encode(s)  # f1e3c2e5f23a6ba0ab90f4ff
+    for cap in range(0, len(want) + 2):
+        blob = np.frombuffer(s, np.uint8).copy()
+        off = np.array([0, len(s)], np.uint32)
+        oo = np.array([0, cap], np.uint32)
+        out = np.full(cap + 8, 0xAB, np.uint8)
+        ol = np.zeros(1, np.uint32)
+        st = np.zeros(1, np.uint8)
+        assert L.hpk_encode_batch_cpu(blob.ctypes.data, off.ctypes.data, 1, out.ctypes.data, oo.ctypes.data,
+                                      ol.ctypes.data, st.ctypes.data, 1) == 0
+        if cap < len(want):
+            assert st[0] == _lib.HPK_OUTPUT_OVERFLOW and ol[0] == cap, cap
+        else:
+            assert st[0] == 0 and ol[0] == len(want), cap
+        assert out[: ol[0]].tobytes() == want[: ol[0]]
+        assert (out[cap:] == 0xAB).all()
+        buf = ctypes.create_string_buffer(max(cap, 1))
+        n1 = ctypes.c_size_t(99)
+        rc = L.hpk_huffman_encode_one(s, len(s), buf, cap, ctypes.byref(n1))
+        assert rc == (_lib.HPK_E_NOSPACE if cap < len(want) else 0) and n1.value == min(cap, len(want))
+
+
+def test_codec_argument_checks():
+    """The Python layer refuses buffers the C ABI would misread: int64 offsets (read as u32 halves),
+    views, short status/length arrays, host arrays for a device call (no GPU needed)."""
+    from loona_amd.batch import _arg
+
+    torch = pytest.importorskip("torch")
+    ok = np.zeros(10, np.uint32)
+    assert _arg(ok, "in_off", ("int32", "uint32"), 10)[1] == 40
+    with pytest.raises(TypeError):
+        _arg(np.zeros(10, np.int64), "in_off", ("int32", "uint32"), 10)
+    with pytest.raises(TypeError):
+        _arg(torch.zeros(10, dtype=torch.int64), "in_off", ("int32", "uint32"), 10)
+    with pytest.raises(ValueError):
+        _arg(np.zeros(20, np.uint32)[::2], "in_off", ("int32", "uint32"), 10)
+    with pytest.raises(ValueError):
+        _arg(torch.zeros(20, dtype=torch.int32)[::2], "in_off", ("int32", "uint32"), 10)
+    with pytest.raises(ValueError):
+        _arg(np.zeros(3, np.uint8), "status", ("uint8",), 4)
+    with pytest.raises(ValueError):
+        _arg(np.zeros(3, np.uint8), "status", ("uint8",), 3, device_index=0)
+    with pytest.raises(TypeError):
+        _arg([0, 1], "in_off", ("int32", "uint32"), 2)
+
+
+def test_host_offsets_checked_against_capacity():
+    """hpk.h: offsets past a blob's capacity or above HPK_MAX_OFFSET are API errors on the host path
+    (checked before anything is copied) — exercised through the host-side checks with a NULL ctx."""
+    L = _lib.lib()
+    blob = np.zeros(8, np.uint8)
+    off = np.array([0, 4, 8], np.uint32)
+    out = np.zeros(16, np.uint8)
+    oo = np.array([0, 8, 16], np.uint32)
+    ol = np.zeros(2, np.uint32)
+    st = np.zeros(2, np.uint8)
+    # a NULL context is rejected before any buffer is touched
+    assert L.hpk_decode_batch(None, blob.ctypes.data, 8, off.ctypes.data, 2, out.ctypes.data, 16, oo.ctypes.data,
+                              ol.ctypes.data, st.ctypes.data, _lib.HPK_PTR_HOST) == _lib.HPK_E_INVAL
+    assert _lib.HPK_MAX_OFFSET == 0xFFFFFFDF
