@@ -44,85 +44,126 @@ def local_shard(blob, in_off, rank: int, world: int):
     return shard(blob, in_off, int(b[rank]), int(b[rank + 1]))
 
 
-def _send_array(dist, arr, dst, device, group):
+def _wire(t):
+    """A tensor as it travels: 4-byte offsets/lengths as int32 (uint32 bit-views included), bytes as
+    uint8. RCCL and gloo both carry these; nothing is widened to int64."""
     import torch
 
-    t = torch.from_numpy(np.ascontiguousarray(arr)).to(device)
-    dist.send(t, dst, group=group)
-
-
-def _recv_array(dist, count, dtype, src, device, group):
-    import torch
-
-    t = torch.empty(count, dtype=dtype, device=device)
-    dist.recv(t, src, group=group)
+    if t.dtype == torch.uint32:
+        return t.view(torch.int32)
     return t
 
 
-def scatter_decode_gather(decode_fn, blob=None, in_off=None, group=None, device="cpu", root=0):
+def _p2p(dist, ops, group):
+    if not ops:
+        return
+    reqs = dist.batch_isend_irecv([dist.P2POp(op, t, peer, group) for op, t, peer in ops])
+    for r in reqs:
+        r.wait()
+
+
+def owner(s: int, world: int) -> int:
+    """Rank that decodes shard s (round-robin)."""
+    return s % world
+
+
+def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
     """Root-resident batch -> per-rank shards -> decode_fn on every rank -> results on root.
 
-    decode_fn(blob_u8, off_u32) -> (out_blob u8, out_off u32[m+1], out_len u32[m], status u8[m])
-    runs on each rank's shard (numpy in, numpy out). Returns on root the concatenated
-    (out_blob, out_off, out_len, status) in the original literal order; None elsewhere."""
+    shards (root only; ignored elsewhere): a list of (blob uint8, off int32/uint32 [m+1]) tensors
+    on `device` — a batch already cut into shards of at most 4 GiB each (u32 offsets), e.g. by
+    `balanced_ranges`. Shard s is decoded on rank owner(s, world); root keeps its own.
+    decode_fn(blob, off) -> (out_blob, out_off, out_len, status) tensors on `device`.
+
+    Everything stays in device memory when `device` is a GPU (RCCL point-to-point over xGMI: one
+    grouped send/recv round out, one back; no host copy): the shard sizes go out with one broadcast,
+    the offsets and blob of each shard with one grouped send/recv, the decoded blob, out_off,
+    out_len and status come back the same way. With gloo and CPU tensors the same code runs on the
+    host (tests/test_shard.py). Returns on root the list of (out_blob, out_off, out_len, status)
+    in shard order; None elsewhere."""
     import torch
     import torch.distributed as dist
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    # 1. shard sizes, from root to every rank: [S] then S x (literals, blob bytes)
+    cnt = torch.tensor([len(shards) if rank == root else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(cnt, root, group=group)
+    S = int(cnt.item())
     if rank == root:
-        b = balanced_ranges(in_off, world)
-        shards = [shard(blob, in_off, int(b[r]), int(b[r + 1])) for r in range(world)]
-        for r in range(world):
-            if r == root:
-                continue
-            sb, so = shards[r]
-            _send_array(dist, np.array([len(so) - 1, len(sb)], dtype=np.int64), r, device, group)
-            _send_array(dist, so.astype(np.int64), r, device, group)
-            if len(sb):
-                _send_array(dist, sb, r, device, group)
-        my_blob, my_off = shards[root]
+        meta = torch.tensor([[int(o.numel()) - 1, int(b.numel())] for b, o in shards], dtype=torch.int64,
+                            device=dev).reshape(S, 2)
     else:
-        hdr = _recv_array(dist, 2, torch.int64, root, device, group).cpu().numpy()
-        m, nbytes = int(hdr[0]), int(hdr[1])
-        my_off = _recv_array(dist, m + 1, torch.int64, root, device, group).cpu().numpy().astype(U32)
-        my_blob = (_recv_array(dist, nbytes, torch.uint8, root, device, group).cpu().numpy()
-                   if nbytes else np.zeros(0, np.uint8))
-
-    ob, oo, ol, st = decode_fn(my_blob, my_off)
-    m = len(my_off) - 1
+        meta = torch.empty((S, 2), dtype=torch.int64, device=dev)
+    if S:
+        dist.broadcast(meta, root, group=group)
+    sizes = meta.tolist()
+    mine = [s for s in range(S) if owner(s, world) == rank]
+    # 2. scatter: offsets + blob of each shard to its owner
+    local, ops = {}, []
+    for s in range(S):
+        o = owner(s, world)
+        m, nb = sizes[s]
+        if rank == root and o != root:
+            b, off = shards[s]
+            ops.append((dist.isend, _wire(off), o))
+            if nb:
+                ops.append((dist.isend, b, o))
+        elif rank == o and o != root:
+            off = torch.empty(m + 1, dtype=torch.int32, device=dev)
+            b = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+            ops.append((dist.irecv, off, root))
+            if nb:
+                ops.append((dist.irecv, b[:nb], root))
+            local[s] = (b, off)
+        elif rank == root:
+            local[s] = shards[s]
+    _p2p(dist, ops, group)
+    # 3. decode the local shards
+    res = {s: decode_fn(*local[s]) for s in mine}
+    # 4. gather: output sizes first, then out_off, out_len, status and the decoded blob
+    hdr, ops = {}, []
+    for s in range(S):
+        o = owner(s, world)
+        if o == root:
+            continue
+        if rank == o:
+            ob = res[s][1]
+            hdr[s] = torch.tensor([int(ob[-1].item()) & 0xFFFFFFFF], dtype=torch.int64, device=dev)
+            ops.append((dist.isend, hdr[s], root))
+        elif rank == root:
+            hdr[s] = torch.empty(1, dtype=torch.int64, device=dev)
+            ops.append((dist.irecv, hdr[s], o))
+    _p2p(dist, ops, group)
+    out, ops = {}, []
+    for s in range(S):
+        o = owner(s, world)
+        m = sizes[s][0]
+        if o == root:
+            continue
+        if rank == o:
+            ob, oo, ol, st = res[s]
+            nbytes = int(hdr[s].item())
+            ops += [(dist.isend, _wire(oo[: m + 1]), root), (dist.isend, _wire(ol[:m]), root),
+                    (dist.isend, st[:m], root)]
+            if nbytes:
+                ops.append((dist.isend, ob[:nbytes], root))
+        elif rank == root:
+            nbytes = int(hdr[s].item())
+            oo = torch.empty(m + 1, dtype=torch.int32, device=dev)
+            ol = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+            st = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
+            ob = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+            ops += [(dist.irecv, oo, o), (dist.irecv, ol[:m], o), (dist.irecv, st[:m], o)]
+            if nbytes:
+                ops.append((dist.irecv, ob[:nbytes], o))
+            out[s] = (ob, oo, ol[:m], st[:m])
+    ops = [x for x in ops if x[1].numel()]
+    _p2p(dist, ops, group)
     if rank != root:
-        _send_array(dist, np.array([m, int(oo[-1])], dtype=np.int64), root, device, group)
-        if m:
-            _send_array(dist, np.asarray(oo, np.int64), root, device, group)
-            _send_array(dist, np.asarray(ol, np.int64), root, device, group)
-            _send_array(dist, np.asarray(st, np.uint8), root, device, group)
-            if int(oo[-1]):
-                _send_array(dist, np.asarray(ob[: int(oo[-1])], np.uint8), root, device, group)
         return None
-    parts = []
-    for r in range(world):
-        if r == root:
-            parts.append((ob[: int(oo[-1])], np.asarray(oo, np.int64), np.asarray(ol, np.int64), np.asarray(st)))
-            continue
-        hdr = _recv_array(dist, 2, torch.int64, r, device, group).cpu().numpy()
-        mr, nb = int(hdr[0]), int(hdr[1])
-        if mr == 0:
-            parts.append((np.zeros(0, np.uint8), np.zeros(1, np.int64), np.zeros(0, np.int64), np.zeros(0, np.uint8)))
-            continue
-        roo = _recv_array(dist, mr + 1, torch.int64, r, device, group).cpu().numpy()
-        rol = _recv_array(dist, mr, torch.int64, r, device, group).cpu().numpy()
-        rst = _recv_array(dist, mr, torch.uint8, r, device, group).cpu().numpy()
-        rob = _recv_array(dist, nb, torch.uint8, r, device, group).cpu().numpy() if nb else np.zeros(0, np.uint8)
-        parts.append((rob, roo, rol, rst))
-    # concatenate with rebased output offsets
-    out_blob = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.uint8)
-    base = 0
-    offs = [np.zeros(1, np.int64)]
-    for p in parts:
-        offs.append(p[1][1:] + base)
-        base += int(p[1][-1])
-    out_off = np.concatenate(offs)
-    if out_off[-1] >= 2**32:
-        raise ValueError("gathered output exceeds u32 offsets")
-    return (out_blob, out_off.astype(U32), np.concatenate([p[2] for p in parts]).astype(U32),
-            np.concatenate([p[3] for p in parts]).astype(np.uint8))
+    for s in mine:
+        ob, oo, ol, st = res[s]
+        m = sizes[s][0]
+        out[s] = (ob, oo, ol[:m], st[:m])
+    return [out[s] for s in range(S)]

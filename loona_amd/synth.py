@@ -138,3 +138,166 @@ def config5_shard(n_total=256_000_000, world=8, rank=0, seed=SEED + 5):
     w.name = "config5"
     w.desc = f"rank {rank}/{world}: {per} of {n_total} config-2 literals"
     return w
+
+
+# ---------------------------------------------------------------------------------------------
+# Device-side generation for the full-size configs (config 5's 32M-literal shards, config 3 at
+# 1M): the same distributions as above, drawn with torch's CUDA generator (seeded, deterministic
+# per seed and device type) instead of numpy, and encoded by the library's device encoder into
+# exact-size regions, so a 32M-literal shard (1.15 GB of strings) is made in well under a second.
+# The encoder is parity-tested against the oracle (tests/test_gpu.py); the tests and the bench
+# check every decoded byte against the generated strings.
+
+
+def code_lengths():
+    """Bits of each byte's RFC 7541 code (from the library's encoded-length function)."""
+    L = _lib.lib()
+    return np.array([L.hpk_huffman_encoded_len(bytes([b]) * 8, 8) for b in range(256)], np.int64)
+
+
+class DeviceWorkload:
+    """A batch resident on one GPU: enc_blob/enc_off (the decode input, int32 offsets),
+    dec_blob/dec_off (the generated strings, int64 offsets) as torch tensors."""
+
+    def __init__(self, name, enc_blob, enc_off, dec_blob, dec_off, desc=""):
+        self.name, self.desc = name, desc
+        self.enc_blob, self.enc_off = enc_blob, enc_off
+        self.dec_blob, self.dec_off = dec_blob, dec_off
+        self.n = int(enc_off.shape[0]) - 1
+        self.enc_bytes = int(enc_off[-1].item())
+        self.dec_bytes = int(dec_off[-1].item())
+
+    def drop_strings(self):
+        self.dec_blob = self.dec_off = None
+
+
+def _device_strings(g, lens, uniform_frac, device, chunk=1 << 26):
+    import torch
+
+    p = char_model()
+    cdf = torch.tensor(np.cumsum(p), dtype=torch.float64, device=device)
+    cdf[-1] = 2.0  # every u < 1 maps to a byte
+    off = torch.zeros(lens.numel() + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, 0, out=off[1:])
+    total = int(off[-1].item())
+    blob = torch.empty(total, dtype=torch.uint8, device=device)
+    for s in range(0, total, chunk):
+        m = min(chunk, total - s)
+        u = torch.rand(m, generator=g, device=device, dtype=torch.float64)
+        part = torch.searchsorted(cdf, u, right=True).clamp_(max=255).to(torch.uint8)
+        if uniform_frac > 0:
+            mask = torch.rand(m, generator=g, device=device) < uniform_frac
+            part[mask] = torch.randint(0, 256, (int(mask.sum().item()),), generator=g, device=device,
+                                       dtype=torch.int64).to(torch.uint8)
+        blob[s : s + m] = part
+    return blob, off
+
+
+def _device_encode(codec, dec_blob, dec_off, chunk=1 << 26):
+    """Exact encoded lengths (sums of code lengths, device cumsums per chunk of literals), then one
+    device encode into regions of exactly that size."""
+    import torch
+
+    dev = dec_blob.device
+    lens_tab = torch.tensor(code_lengths(), dtype=torch.int64, device=dev)
+    n = dec_off.numel() - 1
+    bits = torch.empty(n, dtype=torch.int64, device=dev)
+    # literal ranges of about `chunk` bytes
+    cuts = torch.searchsorted(dec_off, torch.arange(0, int(dec_off[-1].item()) + chunk, chunk, device=dev)).tolist()
+    cuts = sorted(set([0] + [min(c, n) for c in cuts] + [n]))
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if a == b:
+            continue
+        x0, x1 = int(dec_off[a].item()), int(dec_off[b].item())
+        cs = torch.zeros(x1 - x0 + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens_tab[dec_blob[x0:x1].to(torch.int64)], 0, out=cs[1:])
+        o = dec_off[a : b + 1] - x0
+        bits[a:b] = cs[o[1:]] - cs[o[:-1]]
+    enc_len = (bits + 7) // 8
+    enc_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(enc_len, 0, out=enc_off[1:])
+    if int(enc_off[-1].item()) >= 2**31 or int(dec_off[-1].item()) >= 2**31:
+        raise ValueError("device workloads keep int32 offsets: shard too large")
+    enc_off32 = enc_off.to(torch.int32)
+    enc_blob = torch.empty(max(int(enc_off[-1].item()), 1), dtype=torch.uint8, device=dev)
+    ol = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    codec.encode_into(dec_blob, dec_off.to(torch.int32), enc_blob, enc_off32, ol, st, device=True, sync=True)
+    if st.any().item() or not torch.equal(ol.to(torch.int64), enc_len):
+        raise RuntimeError("device encode of the synthetic batch disagrees with the code-length sums")
+    return enc_blob, enc_off32
+
+
+def device_config2(codec, n=1_000_000, seed=SEED, device="cuda"):
+    """Config-2 distribution (decoded length U[8,64], fixture character model) made on the GPU."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    lens = torch.randint(8, 65, (n,), generator=g, device=device, dtype=torch.int64)
+    dec_blob, dec_off = _device_strings(g, lens, 0.0, device)
+    enc_blob, enc_off = _device_encode(codec, dec_blob, dec_off)
+    return DeviceWorkload("config2", enc_blob, enc_off, dec_blob, dec_off,
+                          desc=f"{n} short literals, decoded len U[8,64], fixture char model (device-generated)")
+
+
+def device_config3(codec, n=1_000_000, seed=SEED + 3, device="cuda"):
+    """Config-3 distribution (Zipf(1.1) lengths 8..4096, 5 % uniform bytes) made on the GPU."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    k = np.arange(8, 4097, dtype=np.float64)
+    w = torch.tensor(1.0 / np.power(k - 7, 1.1), dtype=torch.float64, device=device)
+    lens = torch.multinomial(w, n, replacement=True, generator=g) + 8
+    dec_blob, dec_off = _device_strings(g, lens, 0.05, device)
+    enc_blob, enc_off = _device_encode(codec, dec_blob, dec_off)
+    return DeviceWorkload("config3", enc_blob, enc_off, dec_blob, dec_off,
+                          desc=f"{n} mixed literals, Zipf(1.1) 8..4096, 5% uniform bytes (device-generated)")
+
+
+CONFIG5_TOTAL = 256_000_000
+CONFIG5_SHARDS = 8  # 32M literals each: one launch's u32-offset shard
+
+
+def config5_shard_seed(s):
+    return SEED + 5000 + s
+
+
+def device_config5_shard(codec, s, device="cuda"):
+    """Shard s (0..7) of config 5: 32M config-2-distribution literals, the same data whichever GPU
+    of however many makes it (seeded by the shard index)."""
+    w = device_config2(codec, CONFIG5_TOTAL // CONFIG5_SHARDS, seed=config5_shard_seed(s), device=device)
+    w.name = "config5"
+    w.desc = f"config-5 shard {s}/{CONFIG5_SHARDS}: {w.n} config-2 literals (device-generated)"
+    return w
+
+
+def gather_output(out_blob, out_off, out_len, a, b):
+    """Decoded bytes of literals [a, b) of a device decode, concatenated (torch, on the device)."""
+    import torch
+
+    ln = out_len[a:b].to(torch.int64)
+    st = out_off[a:b].to(torch.int64) & 0xFFFFFFFF
+    tot = int(ln.sum().item())
+    if tot == 0:
+        return torch.zeros(0, dtype=torch.uint8, device=out_blob.device)
+    excl = torch.cumsum(ln, 0) - ln
+    idx = torch.repeat_interleave(st - excl, ln) + torch.arange(tot, device=out_blob.device)
+    return out_blob[idx]
+
+
+def check_decoded(w, out_blob, out_off, out_len, status, chunk=1 << 22):
+    """Every literal decoded OK and every decoded byte equals the generated string (device-side)."""
+    import torch
+
+    if status[: w.n].any().item():
+        raise AssertionError("a literal of the synthetic batch did not decode OK")
+    want_len = (w.dec_off[1:] - w.dec_off[:-1])
+    if not torch.equal(out_len[: w.n].to(torch.int64), want_len):
+        raise AssertionError("decoded lengths differ from the generated strings")
+    for a in range(0, w.n, chunk):
+        b = min(w.n, a + chunk)
+        got = gather_output(out_blob, out_off, out_len, a, b)
+        if not torch.equal(got, w.dec_blob[int(w.dec_off[a].item()) : int(w.dec_off[b].item())]):
+            raise AssertionError(f"decoded bytes differ from the generated strings in literals [{a}, {b})")

@@ -15,17 +15,19 @@ import sys
 
 root = sys.argv[1]
 literals = int(sys.argv[2]) if len(sys.argv) > 2 else None
+workload = sys.argv[3] if len(sys.argv) > 3 else None
+kname = sys.argv[4] if len(sys.argv) > 4 else "hpk_decode"
 vals = collections.defaultdict(list)
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "hpk_decode" not in r["Kernel_Name"]:
+        if kname not in r["Kernel_Name"]:
             continue
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 mean = {k: sum(v) / len(v) for k, v in vals.items()}
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from loona_amd import _lib  # noqa: E402
 
-out = {"kernel": "hpk_decode", "kernel_version": _lib.lib().hpk_version().decode(), "literals": literals, "dispatches": {k: len(v) for k, v in vals.items()}, "raw_mean": mean}
+out = {"kernel": kname, "workload": workload, "kernel_version": _lib.lib().hpk_version().decode(), "literals": literals, "dispatches": {k: len(v) for k, v in vals.items()}, "raw_mean": mean}
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     rd = mean["FETCH_SIZE"] * 1024 * 2
     wr = mean["WRITE_SIZE"] * 1024

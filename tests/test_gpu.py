@@ -441,3 +441,66 @@ def test_bad_device_offsets(codec, kind):
     assert (st.cpu().numpy() == _lib.HPK_BAD_OFFSETS).any()
     g = ebig.cpu().numpy()
     assert (g[:guard] == 0xAB).all() and (g[-guard:] == 0xAB).all()
+
+
+def _prefix_host(out, oo, ol, st, k):
+    """The first k literals of a device decode as numpy (out_blob, out_off, out_len, status)."""
+    end = int(oo[k].item()) & 0xFFFFFFFF
+    return (out[:end].cpu().numpy(), oo[: k + 1].cpu().numpy().view(np.uint32).copy(),
+            ol[:k].cpu().numpy().view(np.uint32).copy(), st[:k].cpu().numpy())
+
+
+def _device_decode(codec, w):
+    from loona_amd.batch import decode_offsets_torch
+
+    oo = decode_offsets_torch(w.enc_off)
+    out = torch.empty((int(oo[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device="cuda")
+    ol = torch.empty(w.n, dtype=torch.int32, device="cuda")
+    st = torch.empty(w.n, dtype=torch.uint8, device="cuda")
+    codec.decode_into(w.enc_blob, w.enc_off, out, oo, ol, st, device=True, sync=True)
+    return out, oo, ol, st
+
+
+def _check_encode_prefix(w, k):
+    """Device encode (the workload's encoded literals) == oracle encode on the first k strings."""
+    dec_off = w.dec_off[: k + 1].cpu().numpy().astype(np.uint32)
+    dec_blob = w.dec_blob[: int(dec_off[-1])].cpu().numpy()
+    want = oracle_encode_batch(dec_blob, dec_off)
+    enc_off = w.enc_off[: k + 1].cpu().numpy().view(np.uint32)
+    got = (w.enc_blob[: int(enc_off[-1])].cpu().numpy(), enc_off, np.diff(enc_off.astype(np.int64)).astype(np.uint32),
+           np.zeros(k, np.uint8))
+    compare_batches(got, want, "device encode vs oracle")
+
+
+def test_config5_shard_full(codec):
+    """One config-5 shard at full size: 32M distinct seeded literals (870 MB encoded), the unit of one
+    bench launch. Every status, length and decoded byte against the generated strings; the first
+    100k literals' decode and encode against the oracle."""
+    from loona_amd import synth
+
+    w = synth.device_config5_shard(codec, 0)
+    assert w.n == 32_000_000 and w.enc_bytes > 800_000_000
+    out, oo, ol, st = _device_decode(codec, w)
+    synth.check_decoded(w, out, oo, ol, st)
+    k = 100_000
+    eo = w.enc_off[: k + 1].cpu().numpy().view(np.uint32)
+    want = oracle_decode_batch(w.enc_blob[: int(eo[-1])].cpu().numpy(), eo)
+    compare_batches(_prefix_host(out, oo, ol, st, k), want, "config5 shard prefix vs oracle")
+    _check_encode_prefix(w, k)
+
+
+def test_config3_full_roundtrip(codec):
+    """BASELINE config 3 at full size (1M literals, Zipf lengths to 4 KiB, 5 % uniform bytes):
+    device encode -> device decode gives back every generated byte; device encode == oracle encode
+    and device decode == oracle decode on the first 100k literals."""
+    from loona_amd import synth
+
+    w = synth.device_config3(codec)
+    assert w.n == 1_000_000 and w.dec_bytes > 300_000_000
+    out, oo, ol, st = _device_decode(codec, w)
+    synth.check_decoded(w, out, oo, ol, st)
+    k = 100_000
+    _check_encode_prefix(w, k)
+    eo = w.enc_off[: k + 1].cpu().numpy().view(np.uint32)
+    want = oracle_decode_batch(w.enc_blob[: int(eo[-1])].cpu().numpy(), eo)
+    compare_batches(_prefix_host(out, oo, ol, st, k), want, "config3 prefix vs oracle")

@@ -54,37 +54,67 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, seed, q):
+def _cpu_decode(b, o):
+    """The library's CPU batch path on torch CPU tensors (u32 offsets travel as int32 views)."""
+    import torch
+
+    ob, oo, ol, st = decode_batch_cpu(b.numpy(), o.numpy().view(np.uint32), nthreads=2)
+    return (torch.from_numpy(ob), torch.from_numpy(oo.view(np.int32)), torch.from_numpy(ol.view(np.int32)),
+            torch.from_numpy(st))
+
+
+def _worker(rank, world, port, n, seed, nshards, q):
+    import torch
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        blob = off = None
+        shards = None
         if rank == 0:
             blob, off = _lits(n, seed)
-        res = shard.scatter_decode_gather(lambda b, o: decode_batch_cpu(b, o, nthreads=2), blob, off)
+            b = shard.balanced_ranges(off, nshards)
+            shards = []
+            for r in range(nshards):
+                sb, so = shard.shard(blob, off, int(b[r]), int(b[r + 1]))
+                shards.append((torch.from_numpy(np.ascontiguousarray(sb)), torch.from_numpy(so.view(np.int32))))
+        res = shard.scatter_decode_gather(shards, _cpu_decode)
         if rank == 0:
-            q.put(tuple(np.asarray(x) for x in res))
+            q.put([tuple(x.numpy() for x in r) for r in res])
+        else:
+            assert res is None
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_scatter_decode_gather_gloo(world):
+@pytest.mark.parametrize("world,nshards", [(2, 5), (3, 3)])
+def test_scatter_decode_gather_gloo(world, nshards):
+    """Root-resident shards -> owners (round-robin) -> decode -> root, over gloo with CPU tensors:
+    the same function bench.py runs over RCCL with device tensors. Root's reassembled results
+    equal the oracle's on the whole batch (an empty shard included when world > shards' data)."""
     import torch.multiprocessing as mp
 
     n, seed = 20000, 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, nshards, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    assert len(res) == nshards
+    # concatenate the shards' results with rebased output offsets
+    out_blob = np.concatenate([r[0][: int(r[1].view(np.uint32)[-1])] for r in res])
+    offs, base = [np.zeros(1, np.int64)], 0
+    for r in res:
+        oo = r[1].view(np.uint32).astype(np.int64)
+        offs.append(oo[1:] + base)
+        base += int(oo[-1])
+    got = (out_blob, np.concatenate(offs).astype(np.uint32), np.concatenate([r[2].view(np.uint32) for r in res]),
+           np.concatenate([r[3] for r in res]))
     blob, off = _lits(n, seed)
-    compare_batches(res, oracle_decode_batch(blob, off), "gathered vs oracle")
+    compare_batches(got, oracle_decode_batch(blob, off), "gathered vs oracle")
