@@ -104,19 +104,19 @@ static const char* g_only = nullptr;  // run only the variant of this name (argv
 
 template <int kMode, int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048,
           int kCoop = 1, int kBlocksPerCu = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 0, int kPredSt = 1,
-          int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1>
+          int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1, int kSegBig = 15, int kSegSmall = 32>
 static void run12(const char* name, Dev& d, const std::vector<uint32_t>& ref_len, const std::vector<uint8_t>& ref_st,
                   const std::vector<uint8_t>& ref_out, int num_cu, int iters) {
     if (g_only && strcmp(g_only, name) != 0) return;
     using G = Geo12<kWaves, kW, kO, kQ>;
-    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead, kEven>, 0, G::kBlock, kBlocksPerCu,
+    run_fn<kMode>(name, hpk_decode12<kMode, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead, kEven, kSegBig, kSegSmall>, 0, G::kBlock, kBlocksPerCu,
                   d, ref_len, ref_st, ref_out, num_cu, iters);
 }
 
 // v12 diagnostic stamps (kMode 3): per wave total cycles, cycles in the decode phases, steps, fills
 template <int kR, int kLook, bool kAcc, int kWaves = 16, int kW = 40960, int kO = 79104, int kQ = 2048, int kSched = 0,
           int kLongDyn = 1, int kDefer = 0, int kPredSt = 1, int kSpread = 0, int kSmallFill = 512, uint32_t kLead = 0,
-          int kEven = 1>
+          int kEven = 1, int kCoop = 1>
 static void stamps12(const char* name, Dev& d, int num_cu) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     const size_t nw = (size_t)num_cu * kWaves;
@@ -124,7 +124,7 @@ static void stamps12(const char* name, Dev& d, int num_cu) {
     CK(hipMalloc(&dbg, nw * 16 * 8));
     DecodeArgs a = d.a;
     a.dbg = dbg;
-    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, 1, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead, kEven>;
+    auto fn = hpk_decode12<3, kWaves, kW, kO, kQ, kR, 64, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, kSpread, kSmallFill, kLead, kEven>;
     for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(num_cu), dim3(G::kBlock), 0, 0, a);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(nw * 16);
@@ -265,6 +265,12 @@ int main(int argc, char** argv) {
                                                                            cu, iters);
         run12<4, 2, 2, false, 16, 40960, 79104, 2048, 1, 1, 1, 1, 0, 1>("snake_pred_checked", d, ref_len, ref_st, ref_out,
                                                                          cu, 1);
+        // v18 segment stream: thresholds (buckets) big / small fill: 15 = 224 B, 32 = 64 B, 40 = 48 B, 48 = 32 B
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 3, 1, 1, 1, 0, 1, 0, 512, 0, 1, 15, 32>("seg_224_64", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<4, 2, 2, false, 16, 40960, 79104, 2048, 3, 1, 1, 1, 0, 1, 0, 512, 0, 1, 15, 32>("seg_224_64_checked", d, ref_len, ref_st, ref_out, cu, 1);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 3, 1, 1, 1, 0, 1, 0, 512, 0, 1, 15, 48>("seg_224_32", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 3, 1, 1, 1, 0, 1, 0, 512, 0, 1, 32, 48>("seg_64_32", d, ref_len, ref_st, ref_out, cu, iters);
+        run12<0, 2, 2, false, 16, 40960, 79104, 2048, 3, 1, 1, 1, 0, 1, 0, 512, 0, 1, 24, 40>("seg_128_48", d, ref_len, ref_st, ref_out, cu, iters);
         // two 512-thread workgroups per CU (<= 80 KiB of LDS each): one workgroup's fill setup,
         // barrier wait and write-back overlap the other's decode
         run12<0, 2, 2, false, 8, 18432, 32096, 1024, 1, 2, 1>("wg2_w18", d, ref_len, ref_st, ref_out, cu, iters);
@@ -277,6 +283,7 @@ int main(int argc, char** argv) {
             stamps12<2, 2, false, 16, 40960, 79104, 2048, 1>("coop1_snake", d, cu);
             stamps12<2, 2, false, 16, 40960, 79104, 2048, 1, 1, 0, 1, 0, 512, 0>("snake_nolead", d, cu);
             stamps12<2, 2, false, 16, 40960, 79104, 2048, 1, 0>("snake_longstatic", d, cu);
+            stamps12<2, 2, false, 16, 40960, 79104, 2048, 1, 1, 0, 1, 0, 512, 0, 1, 3>("seg_224_64", d, cu);
         }
         return 0;
     }

@@ -527,6 +527,283 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 }
 
 // ------------------------------------------------------------------------------------------
+// (v18 segment stream, below) Symbols of a walk: byte k at bits 8(k % 8) of lo (k < 8) or of hi.
+// OR the (<= 2) bytes v in at byte index cnt (0..13) of the 128-bit (lo, hi).
+__device__ __forceinline__ void st128_put(uint64_t& lo, uint64_t& hi, uint32_t cnt, uint32_t v) {
+    const uint32_t sh = cnt * 8u;
+    const uint64_t x = (uint64_t)v;
+    lo |= sh < 64u ? x << (sh & 63u) : 0ull;
+    hi |= sh >= 64u ? x << ((sh - 64u) & 63u) : (sh > 48u ? x >> ((64u - sh) & 63u) : 0ull);
+}
+
+__device__ __forceinline__ void shr128(uint64_t& lo, uint64_t& hi, uint32_t s) {  // s: bits, < 128
+    const uint64_t l = s == 0u ? lo : (s < 64u ? (lo >> (s & 63u)) | (hi << ((64u - s) & 63u)) : hi >> ((s - 64u) & 63u));
+    const uint64_t h = s < 64u ? hi >> (s & 63u) : 0ull;
+    lo = l;
+    hi = h;
+}
+
+__device__ __forceinline__ void shl128(uint64_t& lo, uint64_t& hi, uint32_t s) {  // s: bits, < 128
+    const uint64_t h = s == 0u ? hi : (s < 64u ? (hi << (s & 63u)) | (lo >> ((64u - s) & 63u)) : lo << ((s - 64u) & 63u));
+    const uint64_t l = s < 64u ? lo << (s & 63u) : 0ull;
+    lo = l;
+    hi = h;
+}
+
+// One lane's walk over the segment [s0, e) of a literal at window bit P0 with N bits, from bit b
+// (s0 <= b <= N, b < s0 + 30). Each step reads the LUT2 entry AND the leading-ones entry of the
+// same 32 window bits (both from the window bits, so the reads issue together and a 13..30-bit
+// code costs no branch). Out: where and how it stopped (pos, stop: SegStop), the symbols (cnt of
+// them, in lo/hi, which must be zero on entry) and the code starts it passed (mask, bit i = s0 + i).
+// kJoin: stop at the first code start that the walk of mask `omask` also passed (joined = true,
+// pos = that start, jq = that walk's symbols before it).
+template <bool kJoin>
+__device__ __forceinline__ void walk2(const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                      const uint16_t* __restrict__ lo_tab, uint32_t P0, uint32_t N, uint32_t s0,
+                                      uint32_t b, uint32_t e, uint32_t& pos_o, uint32_t& stop_o, uint32_t& cnt_o,
+                                      uint64_t& mask_o, uint64_t& lo, uint64_t& hi, uint64_t omask, bool& joined,
+                                      uint32_t& jq) {
+    uint32_t pos = b, stop = kThrough, cnt = 0;
+    uint64_t mask = 0;
+    joined = false;
+    jq = 0;
+    WinCur c;
+    wc_load(c, win32, P0 + b);
+    bool run = b < e;
+    // every step takes a code or stops, and a segment of <= 64 bits holds <= 13 codes
+    for (uint32_t guard = 0; run; ++guard) {
+        if (guard > 64u) {
+            stop = kStuck;
+            break;
+        }
+        const uint32_t i0 = pos - s0;  // < 64
+        if (kJoin && ((omask >> i0) & 1ull)) {
+            joined = true;
+            jq = (uint32_t)__popcll(omask & ((1ull << i0) - 1ull));
+            break;
+        }
+        mask |= 1ull << i0;
+        const uint32_t d3 = wc_next(win32, c);
+        const uint32_t w = wc_bits(c);
+        const uint32_t rem = N - pos;
+        const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+        const uint32_t kk = __clz(~w);
+        const uint32_t el = lo_tab[min(kk, (uint32_t)HPK_LO_RUNS - 1u) * 32u + ((w << ((kk + 1u) & 31u)) >> 27)];
+        const uint32_t l1 = (e1 >> 8) & 31u, t1 = (e1 >> 24) & 31u;
+        const bool ok1 = (e1 >= HPK_LUT2_ONE) & (l1 <= rem);
+        const uint32_t i2 = i0 + l1;
+        bool ok2 = ok1 & (e1 >= HPK_LUT2_TWO) & (t1 <= rem) & (s0 + i2 < e);  // the second code starts in the segment
+        bool jn2 = false;
+        if (kJoin) {
+            jn2 = ok2 & (((omask >> (i2 & 63u)) & 1ull) != 0ull);
+            ok2 &= !jn2;
+        }
+        const bool eos = (kk >= (uint32_t)HPK_LO_RUNS) | ((el & 0x1FFu) == HPK_EOS);
+        const uint32_t llen = eos ? 30u : (el >> 9);
+        const bool lng = !ok1 & (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);  // a 13..30-bit code (or EOS)
+        const bool lok = lng & !eos & (llen <= rem);
+        const uint32_t v = ok1 ? (ok2 ? ((e1 & 0xFFu) | ((e1 >> 8) & 0xFF00u)) : (e1 & 0xFFu)) : (lok ? (el & 0xFFu) : 0u);
+        st128_put(lo, hi, cnt, v);
+        cnt += ok1 ? (ok2 ? 2u : 1u) : (lok ? 1u : 0u);
+        if (ok2) mask |= 1ull << i2;
+        const bool stopped = !ok1 & !lok;
+        // stopped: EOS decoded (huffman.rs:112-116), or the next code does not fit (the end: padding)
+        stop = stopped ? ((lng & eos & (llen <= rem)) ? (uint32_t)kEos : (uint32_t)kEnded) : (uint32_t)kThrough;
+        const uint32_t adv = ok1 ? (ok2 ? t1 : l1) : (lok ? llen : 0u);
+        pos += adv;
+        wc_adv(c, adv, d3);
+        if (kJoin && jn2) {
+            joined = true;
+            jq = (uint32_t)__popcll(omask & ((1ull << i2) - 1ull));
+            break;
+        }
+        run = !stopped & (pos < e);
+    }
+    pos_o = pos;
+    stop_o = stop;
+    cnt_o = cnt;
+    mask_o = mask;
+}
+
+__device__ __forceinline__ void store8p(uint8_t* __restrict__ out8, bool ok, uint32_t pos, uint32_t v, uint32_t dmy,
+                                        uint32_t oend, int kStore) {
+    if (kStore == kPred)
+        out8[ok ? pos : dmy] = (uint8_t)v;
+    else if (ok)
+        put8(out8, pos, v, oend, kStore);
+}
+
+// ------------------------------------------------------------------------------------------
+// v18 segment stream (kCoop 3): the queue's head (the fill's longer literals) decoded by whole
+// waves as ONE stream of 64-bit segments. A wave takes literals from the queue one after another
+// and lays their segments side by side over its 64 lanes, chunk after chunk, so a literal's tail
+// and the next literals share a chunk and every lane walks a segment. Within a chunk the lanes of
+// one literal are contiguous; the first lane of a literal starts at a true code boundary (bit 0, or
+// where the literal's previous chunk stopped). The others start speculatively at their segment
+// start and resynchronise: lane j's true start is lane j-1's stop when that came through its
+// segment. The lane then re-walks from there until it meets a code start of its current walk
+// (join; at once when that walk passed the true start): its symbols are the re-walk's followed by
+// the current walk's from the join on, and its stop stays. A lane whose re-walk never joins has a
+// new stop, which corrects its right neighbour in the next round. A first lane's start is true, so
+// round r fixes the literal's r-th lane at the latest; Huffman walks fall into step within a few
+// codes, so most lanes join in round 1 after a few codes. Nothing is walked twice to write: a lane
+// keeps its <= 13 symbols in registers; an exclusive scan of the counts gives its place in the
+// image. A literal's end lane (its first lane that does not come through) writes its length and
+// status; a literal still going at the chunk's end continues, at its true stop, in the wave's next
+// chunk.
+template <int kStore>
+__device__ __forceinline__ void seg_stream(const uint2* __restrict__ q, uint32_t nq, uint32_t* ctr,
+                                           const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                           const uint16_t* __restrict__ lo_tab, uint8_t* __restrict__ out8, uint32_t dmy,
+                                           uint32_t* __restrict__ lenst, unsigned long long& nround,
+                                           unsigned long long& nchunk) {
+    const uint32_t j = threadIdx.x & 63u;
+    // the wave's open literal, segments still to assign (wave-uniform, scalar registers)
+    uint32_t c_ex = 0, c_ey = 0, c_nseg = 0, c_next = 0, c_opos = 0, c_base = 0;
+    bool open = false, qdone = false;
+    for (;;) {  // chunks
+        // 1. lanes -> (literal, segment): the open literal's next segments, then new literals
+        uint32_t fill = 0;
+        uint32_t l_ex = 0, l_ey = 0, s0 = 0, b = 0, l_f = j, l_last = j, l_base = 0;
+        uint32_t l_flags = 0;  // 1: has a segment, 2: the literal's first lane here, 4: more segments follow
+        while (fill < 64u) {
+            if (!open) {
+                if (qdone) break;
+                uint32_t t = 0;
+                if (j == 0) t = atomicAdd(ctr, 1u);
+                t = (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+                if (t >= nq) {
+                    qdone = true;
+                    break;
+                }
+                c_ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)q[t].x);
+                c_ey = (uint32_t)__builtin_amdgcn_readfirstlane((int)q[t].y);
+                if (c_ey & kQ7Byte) continue;  // capacity below the bound: the byte pass
+                c_nseg = ((c_ex >> 16) * 8u + 63u) >> 6;
+                c_next = 0;
+                c_opos = 0;
+                c_base = 0;
+                open = c_nseg != 0;
+                if (!open) {  // an empty literal (not expected here): length 0, status OK
+                    if (j == 0) lenst[c_ey & 0xFFFu] = 0;
+                    continue;
+                }
+            }
+            const uint32_t take = min(64u - fill, c_nseg - c_next);
+            if (j >= fill && j < fill + take) {
+                l_ex = c_ex;
+                l_ey = c_ey;
+                s0 = (c_next + (j - fill)) * 64u;
+                b = j == fill ? c_base : s0;
+                l_f = fill;
+                l_last = fill + take - 1u;
+                l_base = c_opos;
+                l_flags = 1u | (j == fill ? 2u : 0u) | (c_next + take < c_nseg ? 4u : 0u);
+            }
+            fill += take;
+            c_next += take;
+            if (c_next == c_nseg) open = false;
+        }
+        if (fill == 0) break;
+        nchunk += 1;
+        const bool l_act = l_flags & 1u, l_ts = l_flags & 2u;
+        // 2. speculative walks (the first lane of each literal from its true start)
+        const uint32_t P0 = (l_ex & 0xFFFFu) * 8u, N = (l_ex >> 16) * 8u;
+        const uint32_t e = s0 + 64u;
+        // the lane's output: A (an bytes: a re-walk's head) then W's symbols from index bq on
+        uint32_t wpos = 0, wstop = kEnded, wcnt = 0, an = 0, bq = 0;
+        uint64_t wmask = 0, wlo = 0, whi = 0, alo = 0, ahi = 0;
+        bool jn;
+        uint32_t jq;
+        if (l_act) walk2<false>(win32, lut, lo_tab, P0, N, s0, b, e, wpos, wstop, wcnt, wmask, wlo, whi, 0ull, jn, jq);
+        bool bad = false;
+        for (uint32_t round = 1;; ++round) {
+            if (round > 65u) {
+                bad = true;
+                break;
+            }
+            const uint32_t lpos = __shfl_up(wpos, 1);
+            const uint32_t lthr = __shfl_up((uint32_t)(wstop == kThrough), 1);
+            const uint32_t nb = (!l_ts && lthr) ? lpos : b;
+            const bool changed = l_act & (nb != b);
+            if (!__any(changed)) break;
+            nround += 1;
+            if (changed) {
+                b = nb;
+                // fold A into W's symbols, then re-walk from nb into A until W's walk is met
+                shr128(wlo, whi, 8u * bq);
+                shl128(wlo, whi, 8u * an);
+                wlo |= alo;
+                whi |= ahi;
+                wcnt = an + wcnt - bq;
+                alo = ahi = 0;
+                uint32_t rpos, rstop, rcnt;
+                uint64_t rmask;
+                walk2<true>(win32, lut, lo_tab, P0, N, s0, nb, e, rpos, rstop, rcnt, rmask, alo, ahi, wmask, jn, jq);
+                if (jn) {  // rpos = the join: W's stop and its boundaries from there on stay
+                    wmask = rmask | (wmask & ~((1ull << (rpos - s0)) - 1ull));
+                    an = rcnt;
+                    bq = jq;
+                } else {
+                    wpos = rpos;
+                    wstop = rstop;
+                    wcnt = rcnt;
+                    wmask = rmask;
+                    wlo = alo;
+                    whi = ahi;
+                    alo = ahi = 0;
+                    an = 0;
+                    bq = 0;
+                }
+            }
+        }
+        // 3. each literal ends in its first lane that does not come through
+        const uint64_t nt = __ballot(!l_act | (wstop != kThrough));
+        const uint64_t ntf = nt >> l_f;
+        const uint32_t endl = ntf ? l_f + (uint32_t)__builtin_ctzll(ntf) : 64u;
+        const bool ends = endl <= l_last || !(l_flags & 4u);  // the literal's end is in this chunk
+        const uint32_t L = endl <= l_last ? endl : l_last;
+        const uint32_t c = (l_act & (j <= L)) ? an + wcnt - bq : 0u;
+        bad |= l_act & (j <= L) & (wstop == kStuck);
+        shr128(wlo, whi, 8u * bq);
+        shl128(wlo, whi, 8u * an);
+        wlo |= alo;
+        whi |= ahi;
+        uint32_t P = c;  // inclusive scan over the wave, then made per literal
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(P, d);
+            if (j >= (uint32_t)d) P += y;
+        }
+        const uint32_t Pf = __shfl(P, (int)(l_f == 0 ? 0u : l_f - 1u));
+        const uint32_t before = l_f == 0 ? 0u : Pf;  // symbols of earlier literals in this chunk
+        const uint32_t o0 = (l_ey >> 12) & 0x1FFFFu;
+        const uint32_t dst = o0 + l_base + (P - c - before);
+#pragma unroll
+        for (int i = 0; i < 13; ++i) {
+            const uint32_t v = (uint32_t)((i < 8 ? wlo >> (8 * i) : whi >> (8 * (i - 8))) & 0xFFull);
+            store8p(out8, (uint32_t)i < c, dst + (uint32_t)i, v, dmy, o0 + N / 5u, kStore);
+        }
+        if (l_act & ends & (j == L)) {
+            const uint32_t st = bad ? 0x7Fu
+                                    : (wstop == kEos ? (uint32_t)HPK_EOS_IN_STRING
+                                                     : residual_status(N - wpos, win_at(win32, P0 + wpos)));
+            lenst[l_ey & 0xFFFu] = (l_base + P - before) | (st << 24);
+        }
+        // 4. the literal at the chunk's end, if it goes on: its true stop and bytes so far
+        if (open) {
+            const bool go_on = (uint32_t)__builtin_amdgcn_readlane((int)(ends ? 0u : 1u), 63) != 0u;
+            if (go_on) {
+                c_base = (uint32_t)__builtin_amdgcn_readlane((int)wpos, 63);
+                c_opos = (uint32_t)__builtin_amdgcn_readlane((int)(l_base + P - before), 63);
+            } else {
+                open = false;  // it ended early (an error): its remaining segments are not decoded
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 
 // kMode: 0 product; diagnostics (never the default): 1 no decode (fill structure only), 2 no
 // output stores, 3 product + 16 per-wave stamps in a.dbg (cycles: total, in the decode loops,
@@ -551,7 +828,7 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
 // kEven: 1 = fills of about equal input size (fewest the window allows), 0 = greedy full windows.
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
           int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1, int kSpread = 0,
-          int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1>
+          int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1, int kSegBig = 15, int kSegSmall = 32>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -839,7 +1116,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             if (pos[r] != 0xFFFFFFFFu) s_q[s_bbase[pos[r] >> 16] + (pos[r] & 0xFFFFu)] = make_uint2(ex[r], ey[r]);
         // the queue's head goes to whole waves: literals of >= 224 bytes; in a fill of few literals
         // (long ones fill the window: lanes would idle) also those of >= 64 bytes (kSmallFill)
-        const uint32_t lb = (kSmallFill && k <= (uint32_t)kSmallFill) ? 32u : kLongBuckets;
+        // (kCoop 3, the segment stream: literals of the first kSegBig buckets, kSegSmall in a small fill;
+        // bucket b < 48 holds encoded lengths >= 2 (48 - b) + ... : 15 = >= 224 B, 32 = >= 64 B, 48 = >= 32 B)
+        const uint32_t lb = kCoop == 3 ? ((kSmallFill && k <= (uint32_t)kSmallFill) ? (uint32_t)kSegSmall : (uint32_t)kSegBig)
+                                       : ((kSmallFill && k <= (uint32_t)kSmallFill) ? 32u : kLongBuckets);
         const uint32_t nlong = kCoop ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_bbase[lb]) : 0u;
         // the next fill's offsets and window: in flight during this fill's decode. Unconditional
         // (clamped past the range end), so no register phi forces a wait on the stores below.
@@ -881,7 +1161,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         // holding the write-back registers is a separate code path: long_decode never runs with
         // them live, and the decode keeps its registers)
         auto long_phase = [&]() {
-            if (kMode != 1 && nlong) {
+            if (kCoop == 3 && kMode != 1 && nlong) {
+                seg_stream<kStore>(s_q, nlong, &s_ctr[4], win32, s_lut, s_lo, s_out, dmy, s_lenst, t_rounds, n_longs);
+            } else if (kMode != 1 && nlong) {
                 const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
                 for (uint32_t jl = wv; jl < nlong;) {
                     const uint32_t ex = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[jl].x);
@@ -889,7 +1171,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     if (!(ey & kQ7Byte)) {  // (capacity below the bound: the byte pass below)
                         uint32_t len, st, nr;
                         long_decode<kLead>(win32, s_lut, s_lo, s_out, kStore, (ex & 0xFFFFu) * 8u, (ex >> 16) * 8u,
-                                    (ey >> 12) & 0x1FFFFu, len, st, nr);
+                                           (ey >> 12) & 0x1FFFFu, len, st, nr);
                         if (kMode == 3) {
                             t_rounds += nr;
                             n_longs += 1;

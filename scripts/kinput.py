@@ -18,6 +18,31 @@ if cfg.startswith("interop"):  # the interop corpus' Huffman literals (interop_l
     lits = [x for x in interop_literals() if cfg == "interop" or len(x) >= 224]
     blob, off = pack(lits * (n or 1))
     w = synth.Workload(cfg, blob, off)
+elif cfg == "mixlong":  # long literals with every error path (tests/test_gpu.py test_long_literals' mix)
+    from loona_amd import huffman_encode  # noqa: E402
+    from loona_amd.batch import pack  # noqa: E402
+
+    rng = np.random.default_rng(2025)
+    lits = []
+    for k in rng.integers(224, 6000, size=3000):
+        r = rng.random()
+        if r < 0.4:
+            lits.append(huffman_encode(rng.integers(0, 256, int(k), dtype=np.uint8).tobytes()))
+        elif r < 0.7:
+            lits.append(huffman_encode(rng.choice(np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;, ", np.uint8),
+                                                  int(k)).tobytes()))
+        elif r < 0.85:
+            lits.append(rng.integers(0, 256, int(k), dtype=np.uint8).tobytes())  # random bytes: padding / EOS errors
+        else:
+            body = bytearray(huffman_encode(b"accept-encoding: gzip, deflate" * int(k // 30 + 1)))
+            body[int(rng.integers(0, len(body)))] = 0xFF
+            lits.append(bytes(body))
+        lits.append(rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8).tobytes())
+    lits.append(b"\xff" * 3000)
+    lits.append(huffman_encode(bytes([1]) * 800))
+    lits.append(huffman_encode(bytes(range(256)) * 40))
+    blob, off = pack(lits)
+    w = synth.Workload(cfg, blob, off)
 else:
     w = getattr(synth, cfg)() if n is None else getattr(synth, cfg)(n=n)
 with open(path, "wb") as f:
