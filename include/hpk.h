@@ -199,6 +199,61 @@ int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const uint8_t* b
                            uint32_t nblocks, hpk_blocks_out* out);
 void hpk_blocks_out_free(hpk_blocks_out* out);
 
+/* ---- HTTP/2 framing in front of the block decoder ------------------------
+ * hpk_h2conn is one connection's header-reading state: its HPACK decoder and a HEADERS block still
+ * waiting for CONTINUATION frames. hpk_h2_read_frames takes the bytes received on many
+ * connections — connection c's are bytes[off[c] .. off[c+1]), whole frames (RFC 9113 §4.1:
+ * 24-bit length, type, flags, 31-bit stream id) followed by at most one incomplete frame — and
+ * does what the reference does per connection: the deframer's length check and padding removal
+ * (crates/loona/src/h2/server.rs:290-390; Frame::parse crates/loona-h2/src/lib.rs:397-411), the
+ * HEADERS priority block (server.rs:895-911), CONTINUATION gathering until END_HEADERS and the
+ * concatenation (read_headers, server.rs:1349-1417, 1619-1638; flags lib.rs:139-168). Every
+ * complete header block of every connection is then decoded by ONE hpk_hdec_decode_blocks call
+ * (one Huffman batch through ctx, or the CPU path when ctx is NULL). Other frame types are
+ * skipped. The first connection error stops the connection for this and all later calls (the
+ * reference sends GOAWAY); an HPACK decoding error is HPK_H2_COMPRESSION_ERROR and the
+ * connection's later blocks of the same call are marked skipped. */
+typedef struct hpk_h2conn hpk_h2conn;
+
+typedef enum hpk_h2_error {                   /* H2ConnectionError (crates/loona/src/h2/types.rs:300-370) */
+    HPK_H2_OK = 0,
+    HPK_H2_FRAME_TOO_LARGE = 1,               /* FrameTooLarge                 -> FRAME_SIZE_ERROR  */
+    HPK_H2_PADDED_FRAME_EMPTY = 2,            /* PaddedFrameEmpty              -> FRAME_SIZE_ERROR  */
+    HPK_H2_PADDED_FRAME_TOO_SHORT = 3,        /* PaddedFrameTooShort           -> PROTOCOL_ERROR    */
+    HPK_H2_PRIORITY_PARSE = 4,                /* ReadAndParse(PrioritySpec)    -> PROTOCOL_ERROR    */
+    HPK_H2_HEADERS_INVALID_PRIORITY = 5,      /* HeadersInvalidPriority        -> PROTOCOL_ERROR    */
+    HPK_H2_EXPECTED_CONTINUATION_FRAME = 6,   /* ExpectedContinuationFrame     -> PROTOCOL_ERROR    */
+    HPK_H2_EXPECTED_CONTINUATION_FOR_STREAM = 7, /* ExpectedContinuationForStream -> PROTOCOL_ERROR */
+    HPK_H2_UNEXPECTED_CONTINUATION_FRAME = 8, /* UnexpectedContinuationFrame   -> PROTOCOL_ERROR    */
+    HPK_H2_COMPRESSION_ERROR = 9              /* HpackDecodingError            -> COMPRESSION_ERROR */
+} hpk_h2_error;
+
+typedef struct hpk_h2_block {   /* one complete header block, in connection order */
+    uint32_t conn;              /* index of its connection in the call                        */
+    uint32_t stream_id;
+    uint32_t end_stream;        /* the HEADERS frame's END_STREAM flag                        */
+    uint32_t skipped;           /* 1: after a COMPRESSION_ERROR on its connection: not decoded */
+} hpk_h2_block;
+
+typedef struct hpk_h2_out {
+    hpk_blocks_out hb;          /* hb.blocks[i] / headers of blocks[i] (hpk_hdec_decode_blocks) */
+    hpk_h2_block* blocks;       /* hb.n_blocks entries                                          */
+    int32_t* conn_error;        /* per connection: hpk_h2_error (sticky)                        */
+    uint32_t* conn_consumed;    /* per connection: bytes of whole frames consumed (the rest is an
+                                   incomplete frame: pass it again with more bytes)             */
+    uint32_t n_conns;
+} hpk_h2_out;
+
+hpk_h2conn* hpk_h2conn_create(void);
+void hpk_h2conn_destroy(hpk_h2conn* conn);
+hpk_hdec* hpk_h2conn_decoder(hpk_h2conn* conn);                      /* its HPACK decoder */
+int hpk_h2conn_set_max_frame_size(hpk_h2conn* conn, uint32_t max);  /* our SETTINGS_MAX_FRAME_SIZE */
+int hpk_h2conn_error(const hpk_h2conn* conn);                       /* hpk_h2_error */
+int hpk_h2_error_code(int h2_error);                                /* RFC 9113 §7 code for GOAWAY */
+int hpk_h2_read_frames(hpk_ctx* ctx, hpk_h2conn* const* conns, const uint8_t* bytes, const uint32_t* off,
+                       uint32_t nconn, hpk_h2_out* out);
+void hpk_h2_out_free(hpk_h2_out* out);
+
 /* ---- HPACK header blocks: encode (the response path) ----------------------
  * hpk_henc mirrors hpack::Encoder (crates/loona-hpack/src/encoder.rs:172-335): one per
  * connection, holding the dynamic table, with the reference's single strategy (a header found
@@ -217,6 +272,22 @@ int hpk_henc_set_max_table_size(hpk_henc* enc, size_t max_size); /* encoder.rs:1
  * with *out_len = the size needed and the encoder state unchanged; HPK_E_INVAL on bad arguments. */
 int hpk_henc_encode(hpk_henc* enc, const uint8_t* fields, const uint32_t* field_off, size_t n_headers, uint8_t* out,
                     size_t cap, size_t* out_len);
+
+/* Many responses' header blocks at once: block b encodes headers [hdr_off[b], hdr_off[b+1]) (header j
+ * as in hpk_henc_encode) with encoder encs[b]; the blocks of one encoder are encoded in list order.
+ * The table logic runs on the host; every string literal of every Huffman-coding encoder goes
+ * through ONE hpk_encode_batch on ctx (the CPU batch path when ctx is NULL), and the H-bit form is
+ * used where strictly shorter: the bytes equal hpk_henc_encode's block by block. Results in
+ * library-allocated buffers: block b is bytes[block_off[b] .. block_off[b+1]). */
+typedef struct hpk_henc_out {
+    uint8_t* bytes;
+    size_t len;
+    uint32_t* block_off;
+    uint32_t n_blocks;
+} hpk_henc_out;
+int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const uint8_t* fields, const uint32_t* field_off,
+                           const uint32_t* hdr_off, uint32_t nblocks, hpk_henc_out* out);
+void hpk_henc_out_free(hpk_henc_out* out);
 
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);

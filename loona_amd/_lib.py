@@ -60,10 +60,20 @@ EXPORTS = (
     "hpk_hdec_table_size",
     "hpk_hdec_decode_blocks",
     "hpk_blocks_out_free",
+    "hpk_h2conn_create",
+    "hpk_h2conn_destroy",
+    "hpk_h2conn_decoder",
+    "hpk_h2conn_set_max_frame_size",
+    "hpk_h2conn_error",
+    "hpk_h2_error_code",
+    "hpk_h2_read_frames",
+    "hpk_h2_out_free",
     "hpk_henc_create",
     "hpk_henc_destroy",
     "hpk_henc_set_max_table_size",
     "hpk_henc_encode",
+    "hpk_henc_encode_blocks",
+    "hpk_henc_out_free",
     "hpk_version",
 )
 
@@ -81,6 +91,21 @@ class BlocksOut(ctypes.Structure):
     _fields_ = [("arena", ctypes.POINTER(ctypes.c_uint8)), ("arena_len", ctypes.c_size_t),
                 ("headers", ctypes.POINTER(Header)), ("n_headers", ctypes.c_size_t),
                 ("blocks", ctypes.POINTER(BlockResult)), ("n_blocks", ctypes.c_uint32)]
+
+
+class HencOut(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.POINTER(ctypes.c_uint8)), ("len", ctypes.c_size_t),
+                ("block_off", ctypes.POINTER(ctypes.c_uint32)), ("n_blocks", ctypes.c_uint32)]
+
+
+class H2Block(ctypes.Structure):
+    _fields_ = [("conn", ctypes.c_uint32), ("stream_id", ctypes.c_uint32), ("end_stream", ctypes.c_uint32),
+                ("skipped", ctypes.c_uint32)]
+
+
+class H2Out(ctypes.Structure):
+    _fields_ = [("hb", BlocksOut), ("blocks", ctypes.POINTER(H2Block)), ("conn_error", ctypes.POINTER(ctypes.c_int32)),
+                ("conn_consumed", ctypes.POINTER(ctypes.c_uint32)), ("n_conns", ctypes.c_uint32)]
 
 
 _lock = threading.Lock()
@@ -155,6 +180,23 @@ def lib() -> ctypes.CDLL:
         L.hpk_hdec_decode_blocks.restype = ctypes.c_int
         L.hpk_blocks_out_free.argtypes = [ctypes.POINTER(BlocksOut)]
         L.hpk_blocks_out_free.restype = None
+        L.hpk_h2conn_create.argtypes = []
+        L.hpk_h2conn_create.restype = ctypes.c_void_p
+        L.hpk_h2conn_destroy.argtypes = [ctypes.c_void_p]
+        L.hpk_h2conn_destroy.restype = None
+        L.hpk_h2conn_decoder.argtypes = [ctypes.c_void_p]
+        L.hpk_h2conn_decoder.restype = ctypes.c_void_p
+        L.hpk_h2conn_set_max_frame_size.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.hpk_h2conn_set_max_frame_size.restype = ctypes.c_int
+        L.hpk_h2conn_error.argtypes = [ctypes.c_void_p]
+        L.hpk_h2conn_error.restype = ctypes.c_int
+        L.hpk_h2_error_code.argtypes = [ctypes.c_int]
+        L.hpk_h2_error_code.restype = ctypes.c_int
+        L.hpk_h2_read_frames.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.POINTER(H2Out)]
+        L.hpk_h2_read_frames.restype = ctypes.c_int
+        L.hpk_h2_out_free.argtypes = [ctypes.POINTER(H2Out)]
+        L.hpk_h2_out_free.restype = None
         L.hpk_henc_create.argtypes = [ctypes.c_int]
         L.hpk_henc_create.restype = ctypes.c_void_p
         L.hpk_henc_destroy.argtypes = [ctypes.c_void_p]
@@ -164,6 +206,11 @@ def lib() -> ctypes.CDLL:
         L.hpk_henc_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_void_p, ctypes.c_size_t, c_sizep]
         L.hpk_henc_encode.restype = ctypes.c_int
+        L.hpk_henc_encode_blocks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(HencOut)]
+        L.hpk_henc_encode_blocks.restype = ctypes.c_int
+        L.hpk_henc_out_free.argtypes = [ctypes.POINTER(HencOut)]
+        L.hpk_henc_out_free.restype = None
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

@@ -726,3 +726,131 @@ extern "C" int hpk_henc_encode(hpk_henc* e, const uint8_t* fields, const uint32_
     *e = std::move(next);
     return HPK_E_OK;
 }
+
+// Many response header blocks at once (the batched form of encoder.rs:210-234): the
+// table logic runs per block on the host, in order per encoder (it never depends on how a string
+// is coded); every string literal of every block whose encoder Huffman-codes is then encoded in
+// ONE batch (hpk_encode_batch through ctx, or the library's CPU batch path), and each block is
+// assembled with the H-bit form wherever it is strictly shorter — the same bytes as hpk_henc_encode
+// block by block.
+extern "C" int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const uint8_t* fields,
+                                      const uint32_t* field_off, const uint32_t* hdr_off, uint32_t nblocks,
+                                      hpk_henc_out* out) {
+    if (!encs || !hdr_off || !out) return HPK_E_INVAL;
+    memset(out, 0, sizeof *out);
+    const uint32_t nh = hdr_off[nblocks] - hdr_off[0];
+    for (uint32_t b = 0; b < nblocks; ++b)
+        if (!encs[b] || hdr_off[b + 1] < hdr_off[b]) return HPK_E_INVAL;
+    if (nh && !field_off) return HPK_E_INVAL;
+    for (uint32_t k = 2 * hdr_off[0]; k < 2 * hdr_off[nblocks]; ++k)
+        if (field_off[k + 1] < field_off[k]) return HPK_E_INVAL;
+    if (nh && field_off[2 * hdr_off[nblocks]] > field_off[2 * hdr_off[0]] && !fields) return HPK_E_INVAL;
+    // pass 1: representation of every header; strings to code are recorded as (field start, length)
+    struct Op {
+        uint32_t raw_at, raw_len;  // bytes already final (prefix integers) in `raw`
+        uint32_t str;              // index into the string list, or UINT32_MAX
+    };
+    std::vector<uint8_t> raw;
+    std::vector<Op> ops;
+    std::vector<uint32_t> ops_off(nblocks + 1, 0);
+    std::vector<uint32_t> s_at, s_len;  // string k = fields[s_at[k] .. + s_len[k])
+    std::vector<uint8_t> s_huff;        // its encoder Huffman-codes
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        hpk_henc& e = *encs[b];
+        auto lit = [&](uint32_t at, uint32_t len) {
+            ops.push_back(Op{(uint32_t)raw.size(), 0u, (uint32_t)s_at.size()});
+            s_at.push_back(at);
+            s_len.push_back(len);
+            s_huff.push_back((uint8_t)(e.huffman && len));
+        };
+        for (uint32_t j = hdr_off[b]; j < hdr_off[b + 1]; ++j) {
+            const uint32_t na = field_off[2 * j], nl = field_off[2 * j + 1] - na;
+            const uint32_t va = field_off[2 * j + 1], vl = field_off[2 * j + 2] - va;
+            const uint8_t* nm = fields + na;
+            const uint8_t* v = fields + va;
+            bool full = false;
+            const size_t idx = e.find(nm, nl, v, vl, &full);
+            const uint32_t r0 = (uint32_t)raw.size();
+            if (idx == 0) {  // literal with incremental indexing (encoder.rs:279-291), then add_header
+                raw.push_back(0x40);
+                ops.push_back(Op{r0, 1u, UINT32_MAX});
+                lit(na, nl);
+                lit(va, vl);
+                e.add(std::string((const char*)nm, nl), std::string((const char*)v, vl));
+            } else if (!full) {  // indexed name, value not indexed (encoder.rs:311-323)
+                put_integer(raw, idx, 4, 0x00);
+                ops.push_back(Op{r0, (uint32_t)raw.size() - r0, UINT32_MAX});
+                lit(va, vl);
+            } else {  // indexed (encoder.rs:329-334)
+                put_integer(raw, idx, 7, 0x80);
+                ops.push_back(Op{r0, (uint32_t)raw.size() - r0, UINT32_MAX});
+            }
+        }
+        ops_off[b + 1] = (uint32_t)ops.size();
+    }
+    // pass 2: one Huffman batch for the strings of Huffman-coding encoders
+    const uint32_t ns = (uint32_t)s_at.size();
+    std::vector<uint32_t> bi(ns, UINT32_MAX);  // string -> batch index
+    std::vector<uint32_t> in_off(1, 0), eo(1, 0);
+    std::vector<uint8_t> in;
+    for (uint32_t k = 0; k < ns; ++k) {
+        if (!s_huff[k]) continue;
+        bi[k] = (uint32_t)in_off.size() - 1;
+        in.insert(in.end(), fields + s_at[k], fields + s_at[k] + s_len[k]);
+        in_off.push_back((uint32_t)in.size());
+        eo.push_back(eo.back() + (uint32_t)((hpk_encoded_bound(s_len[k]) + 3) & ~(size_t)3));
+    }
+    const uint32_t nb = (uint32_t)in_off.size() - 1;
+    std::vector<uint8_t> enc(eo.back() ? eo.back() : 1), est(nb ? nb : 1);
+    std::vector<uint32_t> elen(nb ? nb : 1);
+    if (nb) {
+        if (in.empty()) in.push_back(0);
+        const int rc = ctx ? hpk_encode_batch(ctx, in.data(), in.size(), in_off.data(), nb, enc.data(), enc.size(),
+                                              eo.data(), elen.data(), est.data(), HPK_PTR_HOST)
+                           : hpk_encode_batch_cpu(in.data(), in_off.data(), nb, enc.data(), eo.data(), elen.data(),
+                                                  est.data(), 0);
+        if (rc) return rc;
+    }
+    // pass 3: assemble every block
+    std::vector<uint8_t> o;
+    o.reserve(raw.size() + in.size() + 16);
+    out->n_blocks = nblocks;
+    out->block_off = (uint32_t*)malloc((nblocks + 1) * sizeof(uint32_t));
+    if (!out->block_off) return HPK_E_INVAL;
+    out->block_off[0] = 0;
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        for (uint32_t q = ops_off[b]; q < ops_off[b + 1]; ++q) {
+            const Op& op = ops[q];
+            if (op.str == UINT32_MAX) {
+                o.insert(o.end(), raw.begin() + op.raw_at, raw.begin() + op.raw_at + op.raw_len);
+                continue;
+            }
+            const uint32_t k = op.str, n = s_len[k];
+            const uint32_t i = bi[k];
+            if (i != UINT32_MAX && est[i] == HPK_OK && elen[i] < n) {  // the H-bit form, strictly shorter
+                put_integer(o, elen[i], 7, 0x80);
+                o.insert(o.end(), enc.begin() + eo[i], enc.begin() + eo[i] + elen[i]);
+            } else {
+                put_integer(o, n, 7, 0);
+                o.insert(o.end(), fields + s_at[k], fields + s_at[k] + n);
+            }
+        }
+        if (o.size() >= (1ull << 32)) return HPK_E_INVAL;
+        out->block_off[b + 1] = (uint32_t)o.size();
+    }
+    out->len = o.size();
+    out->bytes = (uint8_t*)malloc(o.size() ? o.size() : 1);
+    if (!out->bytes) {
+        hpk_henc_out_free(out);
+        return HPK_E_INVAL;
+    }
+    if (!o.empty()) memcpy(out->bytes, o.data(), o.size());
+    return HPK_E_OK;
+}
+
+extern "C" void hpk_henc_out_free(hpk_henc_out* out) {
+    if (!out) return;
+    free(out->bytes);
+    free(out->block_off);
+    memset(out, 0, sizeof *out);
+}

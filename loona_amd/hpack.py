@@ -27,6 +27,10 @@ The encoder mirrors `hpack::Encoder` (crates/loona-hpack/src/encoder.rs:172-335)
     e = Encoder(huffman=True)           # the H-bit form whenever it is strictly shorter
     e.set_max_table_size(256)           # encoder.rs:193-197
     block = e.encode([(b"custom-key", b"custom-value")])   # encoder.rs:210-217
+
+and its batched form for many responses at once (all their Huffman strings in one device batch):
+
+    encode_blocks([(e1, headers_a), (e2, headers_b), (e1, headers_c)], codec)  # -> [bytes]
 """
 
 from __future__ import annotations
@@ -198,3 +202,34 @@ class Encoder:
                 continue
             _lib.check(rc, "hpk_henc_encode")
             return out[: got.value].tobytes()
+
+
+def encode_blocks(pairs, codec=None):
+    """[(Encoder, [(name, value)])] -> [block bytes]: the table logic per block on the host (blocks of
+    one encoder in list order), every string literal of every Huffman-coding encoder in ONE
+    hpk_encode_batch on `codec`'s device (the library's CPU batch path when codec is None); the same
+    bytes as Encoder.encode block by block (hpk_henc_encode_blocks)."""
+    L = _lib.lib()
+    parts, off, hoff = [], [0], [0]
+    for _, headers in pairs:
+        for name, value in headers:
+            for x in (name, value):
+                parts.append(bytes(x))
+                off.append(off[-1] + len(x))
+        hoff.append(hoff[-1] + len(headers))
+    if off[-1] >= 2**32:
+        raise ValueError("header fields of one call must stay below 4 GiB")
+    fields = np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8).copy()
+    off32 = np.asarray(off, dtype=np.uint32)
+    hoff32 = np.asarray(hoff, dtype=np.uint32)
+    n = len(pairs)
+    encs = (ctypes.c_void_p * max(n, 1))(*[e._h for e, _ in pairs])
+    out = _lib.HencOut()
+    ctx = codec._h if codec is not None else None
+    _lib.check(L.hpk_henc_encode_blocks(ctx, encs, fields.ctypes.data, off32.ctypes.data, hoff32.ctypes.data, n,
+                                        ctypes.byref(out)), "hpk_henc_encode_blocks")
+    try:
+        data = ctypes.string_at(out.bytes, out.len) if out.len else b""
+        return [data[out.block_off[b] : out.block_off[b + 1]] for b in range(n)]
+    finally:
+        L.hpk_henc_out_free(ctypes.byref(out))

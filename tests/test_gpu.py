@@ -504,3 +504,81 @@ def test_config3_full_roundtrip(codec):
     eo = w.enc_off[: k + 1].cpu().numpy().view(np.uint32)
     want = oracle_decode_batch(w.enc_blob[: int(eo[-1])].cpu().numpy(), eo)
     compare_batches(_prefix_host(out, oo, ol, st, k), want, "config3 prefix vs oracle")
+
+
+def test_h2_frames_replay_on_device(codec):
+    """SURVEY §8f-3/§8f-4 through the device: every interop story as HEADERS + CONTINUATION frames
+    (random splits, padding, priority, other frames between blocks, bytes in random chunks over
+    several calls, one connection per story) decodes to the fixtures' header lists with the
+    Huffman batch on the GPU; httpwg's invalid_header_block_fragment
+    (crates/httpwg/src/rfc9113/_4_http_frames.rs:153-169) gives COMPRESSION_ERROR."""
+    from test_h2 import replay
+
+    from loona_amd import h2
+
+    assert replay(codec, seed=11) > 10000
+    c = h2.Connection()
+    r = h2.read_frames([c], [h2.frame(0x1, 0x5, 1, b"\x40")], codec)
+    assert r.errors == ["HpackDecodingError"] and h2.error_code(r.errors[0]) == "COMPRESSION_ERROR"
+
+
+def test_encode_blocks_on_device(codec):
+    """SURVEY §8f-2 through the device: many responses' header blocks with every Huffman string in
+    one device encode batch == the CPU batch path == hpk_henc_encode block by block."""
+    from test_hpack_encoder import response_lists
+
+    from loona_amd import hpack
+
+    lists = response_lists(seed=5)
+    k = 5
+    assert hpack.encode_blocks([], codec) == []
+    encs_d = [hpack.Encoder(huffman=True) for _ in range(k)]
+    encs_s = [hpack.Encoder(huffman=True) for _ in range(k)]
+    got = hpack.encode_blocks([(encs_d[i % k], hs) for i, hs in enumerate(lists)], codec)
+    want = [encs_s[i % k].encode(hs) for i, hs in enumerate(lists)]
+    assert got == want
+
+
+def test_scatter_decode_gather_device_world1(codec):
+    """shard.scatter_decode_gather on device tensors over RCCL ("nccl", world 1: the root keeps every
+    shard): the device-resident path bench.py times at N > 1, results equal the oracle's."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    from loona_amd import shard, synth
+    from loona_amd.batch import decode_offsets_torch
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        w = synth.config2(n=30000, seed=21)
+        b = shard.balanced_ranges(w.enc_off, 3)
+        shards = []
+        for r in range(3):
+            sb, so = shard.shard(w.enc_blob, w.enc_off, int(b[r]), int(b[r + 1]))
+            shards.append((to_dev(sb if sb.size else np.zeros(1, np.uint8)), to_dev(so.view(np.int32))))
+
+        def decode_fn(blob, off):
+            oo = decode_offsets_torch(off)
+            out = torch.empty((int(oo[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device="cuda")
+            ol = torch.empty(max(off.numel() - 1, 1), dtype=torch.int32, device="cuda")
+            st = torch.empty(max(off.numel() - 1, 1), dtype=torch.uint8, device="cuda")
+            codec.decode_into(blob, off, out, oo, ol, st, device=True, sync=False)
+            return out, oo, ol, st
+
+        res = shard.scatter_decode_gather(shards, decode_fn, device="cuda")
+        torch.cuda.synchronize()
+        for r, (ob, oo, ol, st) in enumerate(res):
+            lo, hi = int(b[r]), int(b[r + 1])
+            sb, so = shard.shard(w.enc_blob, w.enc_off, lo, hi)
+            got = (ob.cpu().numpy(), oo.cpu().numpy().view(np.uint32), ol.cpu().numpy().view(np.uint32)[: hi - lo],
+                   st.cpu().numpy()[: hi - lo])
+            compare_batches(got, oracle_decode_batch(sb, so), f"world-1 shard {r}")
+    finally:
+        dist.destroy_process_group()

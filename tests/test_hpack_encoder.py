@@ -124,3 +124,44 @@ def test_nospace_leaves_state_unchanged():
         assert got.value == 1 and out[0] == 0x80 | 62
     finally:
         L.hpk_henc_destroy(h)
+
+
+def response_lists(seed=3, n=3000):
+    """Header lists of the interop stories plus seeded random headers (text, binary, empty)."""
+    import random
+
+    rng = random.Random(seed)
+    inter = load("interop.json.gz")
+    lists = [[(k.encode(), v.encode()) for k, v in c["headers"]] for enc in sorted(inter) for st in inter[enc]
+             for c in st["cases"]]
+    rng.shuffle(lists)
+    lists = lists[:n]
+    for _ in range(200):
+        hs = []
+        for _ in range(rng.randrange(0, 8)):
+            k = rng.choice([b"content-type", b"x-req-id", b"set-cookie", b"server", b":status"])
+            v = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 40))) if rng.random() < 0.3 else \
+                str(rng.randrange(10**9)).encode()
+            hs.append((k, v))
+        lists.append(hs)
+    return lists
+
+
+@pytest.mark.parametrize("huffman", [False, True])
+def test_encode_blocks_matches_block_by_block(huffman):
+    """hpk_henc_encode_blocks (all Huffman strings of all blocks in one batch) == hpk_henc_encode per
+    block, with blocks of several encoders interleaved (each encoder's blocks in order)."""
+    from loona_amd import hpack
+
+    lists = response_lists()
+    k = 7
+    batch_encs = [hpack.Encoder(huffman=huffman) for _ in range(k)]
+    seq_encs = [hpack.Encoder(huffman=huffman) for _ in range(k)]
+    pairs = [(batch_encs[i % k], hs) for i, hs in enumerate(lists)]
+    got = hpack.encode_blocks(pairs, None)
+    want = [seq_encs[i % k].encode(hs) for i, hs in enumerate(lists)]
+    assert got == want
+    # and the blocks decode back to the lists through fresh decoders in the same order
+    decs = [hpack.Decoder() for _ in range(k)]
+    back = hpack.decode_blocks([(decs[i % k], b) for i, b in enumerate(got)], None)
+    assert back == lists
