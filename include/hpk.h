@@ -132,7 +132,8 @@ int hpk_ctx_check(hpk_ctx* ctx);
 /* ---- batch calls on the host CPU ----------------------------------------
  * Same layout and results as the device calls, run by `nthreads` host threads over contiguous
  * literal shards balanced by bytes (thread-per-core, like loona). This is the table-driven CPU
- * path ("cpu-fast" in the bench), not the reference restatement. nthreads <= 0: all cores. */
+ * path ("cpu-fast" in the bench), not the reference restatement. nthreads <= 0: the cores, at most
+ * 16 and at least 2048 literals per thread. */
 int hpk_decode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,
                          const uint32_t* out_off, uint32_t* out_len, uint8_t* status, int nthreads);
 int hpk_encode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_t n, uint8_t* out_blob,

@@ -156,7 +156,12 @@ static int cpu_batch(const uint8_t* in_blob, const uint32_t* in_off, uint32_t n,
         if (in_off[i + 1] < in_off[i] || out_off[i + 1] < out_off[i]) return HPK_E_INVAL;
     if (n == 0) return HPK_E_OK;
     if ((in_off[n] && !in_blob) || (out_off[n] && !out_blob)) return HPK_E_INVAL;
-    if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+    if (nthreads <= 0) {  // default: the cores, at most 16, and >= 2048 literals per thread (a thread's start
+                          // costs more than decoding a few hundred short literals)
+        nthreads = (int)std::thread::hardware_concurrency();
+        if (nthreads > 16) nthreads = 16;
+        if ((uint32_t)nthreads > n / 2048u + 1u) nthreads = (int)(n / 2048u + 1u);
+    }
     if (nthreads < 1) nthreads = 1;
     if ((uint32_t)nthreads > n) nthreads = (int)n;
     auto work = [&](uint32_t lo, uint32_t hi) {
