@@ -146,6 +146,15 @@ int hpk_encode_batch_cpu(const uint8_t* in_blob, const uint32_t* in_off, uint32_
 int hpk_host_register(void* ptr, size_t bytes);
 int hpk_host_unregister(void* ptr);
 
+/* buffet's buffer arena (crates/buffet/src/bufpool/privatepool.rs:80-108: one anonymous mmap of
+ * num_bufs x buf_size, 64Ki x 4 KiB by default there), page-locked when pin != 0, so the frames
+ * and literals read into its buffers DMA straight to the device. NULL on failure. */
+typedef struct hpk_arena hpk_arena;
+hpk_arena* hpk_arena_create(size_t num_bufs, size_t buf_size, int pin);
+void* hpk_arena_base(const hpk_arena* arena);
+size_t hpk_arena_len(const hpk_arena* arena);
+void hpk_arena_destroy(hpk_arena* arena);
+
 /* ---- HPACK header blocks: two-pass decode -----------------------------------------------
  * hpk_hdec mirrors hpack::Decoder (crates/loona-hpack/src/decoder.rs:257-555; header table
  * crates/loona-hpack/src/lib.rs:43-289): one per connection, holding the dynamic table.

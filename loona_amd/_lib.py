@@ -53,6 +53,10 @@ EXPORTS = (
     "hpk_encode_batch_cpu",
     "hpk_host_register",
     "hpk_host_unregister",
+    "hpk_arena_create",
+    "hpk_arena_base",
+    "hpk_arena_len",
+    "hpk_arena_destroy",
     "hpk_hdec_create",
     "hpk_hdec_destroy",
     "hpk_hdec_set_max_table_size",
@@ -166,6 +170,14 @@ def lib() -> ctypes.CDLL:
         L.hpk_host_register.restype = ctypes.c_int
         L.hpk_host_unregister.argtypes = [ctypes.c_void_p]
         L.hpk_host_unregister.restype = ctypes.c_int
+        L.hpk_arena_create.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
+        L.hpk_arena_create.restype = ctypes.c_void_p
+        L.hpk_arena_base.argtypes = [ctypes.c_void_p]
+        L.hpk_arena_base.restype = ctypes.c_void_p
+        L.hpk_arena_len.argtypes = [ctypes.c_void_p]
+        L.hpk_arena_len.restype = ctypes.c_size_t
+        L.hpk_arena_destroy.argtypes = [ctypes.c_void_p]
+        L.hpk_arena_destroy.restype = None
         L.hpk_hdec_create.argtypes = []
         L.hpk_hdec_create.restype = ctypes.c_void_p
         L.hpk_hdec_destroy.argtypes = [ctypes.c_void_p]

@@ -1,6 +1,7 @@
 // hpk_ctx.hip — device context and the batch entry points of the C ABI (include/hpk.h).
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include "hpk_device.h"
 
@@ -256,4 +257,48 @@ extern "C" int hpk_encode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_ca
                                 uint8_t* status, int flags) {
     return run_batch(hpk_launch_encode, c, in_blob, in_cap, in_off, n, out_blob, out_cap, out_off, out_len, status,
                      flags);
+}
+
+// buffet's buffer arena (crates/buffet/src/bufpool/privatepool.rs:80-108): ONE anonymous mapping of
+// num_bufs x buf_size bytes from which a thread's read buffers are carved; page-locked here (pin) so
+// batches whose literal or frame bytes sit in it DMA without a staging copy.
+struct hpk_arena {
+    void* base;
+    size_t len;
+    int pinned;
+};
+
+extern "C" hpk_arena* hpk_arena_create(size_t num_bufs, size_t buf_size, int pin) {
+    if (!num_bufs || !buf_size || num_bufs > ((size_t)1 << 40) / buf_size) {
+        hpk_set_err_msg("bad arena size", HPK_E_INVAL);
+        return nullptr;
+    }
+    const size_t len = num_bufs * buf_size;
+    void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) {
+        hpk_set_err_msg("mmap failed", HPK_E_INVAL);
+        return nullptr;
+    }
+    hpk_arena* a = new hpk_arena{p, len, 0};
+    if (pin) {
+        const hipError_t e = hipHostRegister(p, len, hipHostRegisterDefault);
+        if (e != hipSuccess) {
+            hpk_set_err("hipHostRegister arena", e);
+            munmap(p, len);
+            delete a;
+            return nullptr;
+        }
+        a->pinned = 1;
+    }
+    return a;
+}
+
+extern "C" void* hpk_arena_base(const hpk_arena* a) { return a ? a->base : nullptr; }
+extern "C" size_t hpk_arena_len(const hpk_arena* a) { return a ? a->len : 0; }
+
+extern "C" void hpk_arena_destroy(hpk_arena* a) {
+    if (!a) return;
+    if (a->pinned) (void)hipHostUnregister(a->base);
+    munmap(a->base, a->len);
+    delete a;
 }

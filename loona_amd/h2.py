@@ -73,6 +73,36 @@ class Result:
         self.blocks, self.errors, self.consumed = blocks, errors, consumed
 
 
+class Arena:
+    """buffet's buffer arena (hpk_arena_create: one anonymous mmap of num_bufs x buf_size, page-locked
+    when pin): .view is a writable numpy view of it; read_frames_in() decodes frames in place."""
+
+    def __init__(self, num_bufs=65536, buf_size=4096, pin=True):
+        self._L = _lib.lib()
+        self._h = self._L.hpk_arena_create(num_bufs, buf_size, 1 if pin else 0)
+        if not self._h:
+            raise RuntimeError(f"hpk_arena_create failed: {_lib.last_error()}")
+        n = self._L.hpk_arena_len(self._h)
+        self.base = self._L.hpk_arena_base(self._h)
+        self.view = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(self.base))
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self.view = None
+            self._L.hpk_arena_destroy(h)
+
+    def __del__(self):
+        self.close()
+
+
+def read_frames_in(conns, arena, offsets, codec=None) -> Result:
+    """read_frames on bytes already in an Arena: connection c's bytes are
+    arena.view[offsets[c] : offsets[c+1]] (no copy on the way in)."""
+    off32 = np.ascontiguousarray(offsets, dtype=np.uint32)
+    return _read(conns, arena.base, off32, codec)
+
+
 def read_frames(conns, chunks, codec=None) -> Result:
     """Frames received on each connection (chunks[c] = bytes for conns[c]) -> decoded header blocks."""
     L = _lib.lib()
@@ -84,11 +114,16 @@ def read_frames(conns, chunks, codec=None) -> Result:
     if off[-1] >= 2**32:
         raise ValueError("the bytes of one call must stay below 4 GiB")
     blob = np.frombuffer(b"".join(bytes(c) for c in chunks) or b"\0", dtype=np.uint8).copy()
-    off32 = off.astype(np.uint32)
+    return _read(conns, blob.ctypes.data, off.astype(np.uint32), codec)
+
+
+def _read(conns, base, off32, codec):
+    L = _lib.lib()
+    n = len(conns)
     hs = (ctypes.c_void_p * max(n, 1))(*[c._h for c in conns])
     out = _lib.H2Out()
     ctx = codec._h if codec is not None else None
-    _lib.check(L.hpk_h2_read_frames(ctx, hs, blob.ctypes.data, off32.ctypes.data, n, ctypes.byref(out)),
+    _lib.check(L.hpk_h2_read_frames(ctx, hs, base, off32.ctypes.data, n, ctypes.byref(out)),
                "hpk_h2_read_frames")
     try:
         arena = ctypes.string_at(out.hb.arena, out.hb.arena_len) if out.hb.arena_len else b""

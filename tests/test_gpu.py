@@ -582,3 +582,11 @@ def test_scatter_decode_gather_device_world1(codec):
             compare_batches(got, oracle_decode_batch(sb, so), f"world-1 shard {r}")
     finally:
         dist.destroy_process_group()
+
+
+def test_h2_frames_in_pinned_arena_on_device(codec):
+    """Frames in a page-locked buffet-shaped arena (hpk_arena_create, 64Ki x 4 KiB) decoded in place
+    with the Huffman batch on the device."""
+    from test_h2 import replay_in_arena
+
+    replay_in_arena(codec, pin=True)

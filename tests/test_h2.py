@@ -191,3 +191,29 @@ def test_incomplete_frames_and_pending_continuation_across_calls():
         pos += r.consumed[0]
         got += r.blocks
     assert pos == len(frames) and got == [(0, 1, False, C41)]
+
+
+def replay_in_arena(codec, pin):
+    """The interop connections' frames received into a buffet-shaped arena (64Ki x 4 KiB buffers in
+    one anonymous mapping; the connections' bytes back to back) and decoded in place, all
+    connections in one call."""
+    wires, wants = interop_connections(3)
+    arena = h2.Arena(65536, 4096, pin=pin)
+    try:
+        offs = [0]
+        for w in wires:
+            arena.view[offs[-1] : offs[-1] + len(w)] = memoryview(w)
+            offs.append(offs[-1] + len(w))
+        conns = [h2.Connection() for _ in wires]
+        res = h2.read_frames_in(conns, arena, offs, codec)
+        assert res.errors == [None] * len(wires) and res.consumed == [len(w) for w in wires]
+        got = [[] for _ in wires]
+        for conn, sid, es, val in res.blocks:
+            got[conn].append((sid, es, val))
+        assert got == wants
+    finally:
+        arena.close()
+
+
+def test_replay_in_unpinned_arena_cpu():
+    replay_in_arena(None, pin=False)
