@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.16 gfx950 decode v16 (alignbit step, two lookups per step, unconditional byte stores, static snake schedule, equal-size fills, cooperative long literals with dynamic hand-out, LDS image); encode v2b (segmented scan, run accumulator, LDS image)"
+#define HPK_VERSION "hpk 0.19 gfx950 decode v19 (alignbit step, two lookups per step, unconditional byte stores, static snake schedule, equal-size fills, LDS image; long literals one lane each streaming from HBM in a second kernel); encode v2b (segmented scan, run accumulator, LDS image)"
 
 static thread_local std::string t_last_error;
 
@@ -74,6 +74,37 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     return c;
 }
 
+int hpk_long_state(hpk_ctx* c, uint32_t n, uint32_t** state, uint32_t** list) {
+    int j = -1;
+    for (int k = 0; k < hpk_ctx::kLongSlots; ++k)
+        if (c->long_buf[k] && c->long_stream[k] == c->stream) j = k;
+    if (j < 0) {
+        j = 0;
+        while (j < hpk_ctx::kLongSlots && c->long_buf[j]) ++j;
+        if (j == hpk_ctx::kLongSlots) {  // all taken: reuse the oldest once its stream has drained
+            j = c->long_next;
+            c->long_next = (j + 1) % hpk_ctx::kLongSlots;
+            HIP_TRY(hipStreamSynchronize(c->long_stream[j]));
+        } else {
+            HIP_TRY(hipMalloc(&c->long_buf[j], hpk_ctx::kLongWords * sizeof(uint32_t)));
+        }
+        HIP_TRY(hipMemsetAsync(c->long_buf[j], 0, hpk_ctx::kLongWords * sizeof(uint32_t), c->stream));
+        c->long_stream[j] = c->stream;
+    }
+    if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->long_list[j]);
+        c->long_list[j] = nullptr;
+        c->long_list_cap[j] = 0;
+        const size_t cap = (size_t)n + (n >> 2) + 1024;
+        HIP_TRY(hipMalloc(&c->long_list[j], cap * sizeof(uint32_t)));
+        c->long_list_cap[j] = cap;
+    }
+    *state = c->long_buf[j];
+    *list = c->long_list[j];
+    return HPK_E_OK;
+}
+
 extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -88,6 +119,10 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
+    for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
+        if (c->long_buf[j]) (void)hipFree(c->long_buf[j]);
+        if (c->long_list[j]) (void)hipFree(c->long_list[j]);
+    }
     for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
         if (c->ev_in[j]) (void)hipEventDestroy(c->ev_in[j]);
         if (c->ev_run[j]) (void)hipEventDestroy(c->ev_run[j]);

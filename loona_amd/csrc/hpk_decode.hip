@@ -32,7 +32,7 @@
 // A literal too large for the window is decoded by one lane straight from global memory.
 #include <stdlib.h>
 
-#include "hpk_decode12.h"
+#include "hpk_long.h"
 
 using namespace hpkdec;
 
@@ -42,7 +42,18 @@ using namespace hpkdec;
 // schedule, byte stores into the image (bench/kvariants: profiles/r01/kvariants_v1[23]*.jsonl).
 constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2, kChunk = 64, kLook = 2, kSched = 1;
 constexpr bool kAcc = false;
-constexpr int kCoop = 1;  // literals of >= 224 encoded bytes: one wave each (self-synchronising walk)
+constexpr int kCoop = 0;  // (v16: literals of >= 224 encoded bytes one wave each; v19: hpk_decode_long)
+constexpr int kLongK = 1;  // long literals left to hpk_decode_long
+constexpr int kSpread = 1;  // lane-queue slots interleaved over the waves (fills of few literals use every SIMD)
+#ifndef HPK_LONG_MIN
+#define HPK_LONG_MIN 64  // encoded bytes: literals from here on go to hpk_decode_long
+#endif
+#ifndef HPK_LONG_BIG
+#define HPK_LONG_BIG 1024  // hpk_decode_long takes these first (longest-first, roughly)
+#endif
+// hpk_decode_long: one 512-thread workgroup per CU (2 waves per SIMD), refill every 8 steps, 32-dword
+// input ring per lane
+constexpr int kLongBlock = 512, kLongU = 8, kLongRing = 32;
 using Geo = Geo12<kWaves, kW, kO, kQ>;
 #ifndef HPK_LONGDYN
 #define HPK_LONGDYN 1
@@ -56,7 +67,8 @@ constexpr int kDefer = HPK_DEFER;  // the previous fill's write-back issued duri
 #define HPK_PREDST 1
 #endif
 constexpr int kPredSt = HPK_PREDST;  // unconditional byte stores in the lane step (dummy slots)
-#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt>
+#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, \
+                                   kSpread, 512, 0, 1, 15, 32, kLongK>
 
 #ifdef HPK_DIAG
 // Diagnostic build (libhpk_diag.so, `make diag`; never the product library): HPK_DEBUG_MODE selects
@@ -99,10 +111,22 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
+    uint32_t *ls = nullptr, *ll = nullptr;
+    if (int rc = hpk_long_state(c, b.n, &ls, &ll)) return rc;
+    a.long_wg = ls;
+    a.long_ctr = ls + 512;
+    a.long_list = ll;
+    a.long_min = HPK_LONG_MIN;
+    a.long_big = HPK_LONG_BIG;
+#ifdef HPK_DIAG
+    if (const char* lm = getenv("HPK_LONG_MIN")) a.long_min = (uint32_t)atoi(lm);
+    if (const char* lb = getenv("HPK_LONG_BIG")) a.long_big = (uint32_t)atoi(lb);
+#endif
     // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
+    if (blocks > 256) blocks = 256;  // (long_wg holds 256 counts)
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
 #ifdef HPK_DIAG
     if (g_debug_mode < 0) {
@@ -130,11 +154,53 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
         case 4:
             hipLaunchKernelGGL(DEC_KERNEL(4), grid, block, 0, c->stream, a);
             break;
+        case 5:  // the product kernel; hpk_decode_long with per-wave counters (below)
+            hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
+            break;
         default:
             hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
     }
 #else
     hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
+#endif
+    HIP_TRY(hipGetLastError());
+#ifdef HPK_DIAG
+    // diagnostic variants of hpk_decode_long (HPK_LONG_VAR), with per-wave counters in mode 5
+    static int long_var = -1;
+    if (long_var < 0) {
+        const char* lv = getenv("HPK_LONG_VAR");
+        long_var = lv ? atoi(lv) : 0;
+    }
+    const uint32_t lwaves = long_var == 1 ? 12u : (long_var == 2 ? 4u : 8u);
+    if (g_debug_mode == 5) {
+        const size_t need = (size_t)c->num_cu * lwaves * 16;
+        if (need > g_dbg_n) {
+            (void)hipFree(g_dbg);
+            HIP_TRY(hipMalloc(&g_dbg, need * 8));
+            g_dbg_n = need;
+        }
+        HIP_TRY(hipMemsetAsync(g_dbg, 0, need * 8, c->stream));
+        a.dbg = g_dbg;
+    }
+#define LONG_LAUNCH(B, U, R)                                                                                   \
+    do {                                                                                                        \
+        if (g_debug_mode == 5)                                                                                  \
+            hipLaunchKernelGGL((hpk_decode_long<B, U, R, 1>), dim3((uint32_t)c->num_cu), dim3(B), 0, c->stream, a, \
+                               (uint32_t)blocks);                                                               \
+        else                                                                                                    \
+            hipLaunchKernelGGL((hpk_decode_long<B, U, R, 0>), dim3((uint32_t)c->num_cu), dim3(B), 0, c->stream, a, \
+                               (uint32_t)blocks);                                                               \
+    } while (0)
+    switch (long_var) {
+        case 1: LONG_LAUNCH(768, 8, 16); break;
+        case 2: LONG_LAUNCH(256, 8, 32); break;
+        case 3: LONG_LAUNCH(512, 4, 32); break;
+        case 4: LONG_LAUNCH(512, 16, 32); break;
+        default: LONG_LAUNCH(kLongBlock, kLongU, kLongRing);
+    }
+#else
+    hipLaunchKernelGGL((hpk_decode_long<kLongBlock, kLongU, kLongRing>), dim3((uint32_t)c->num_cu), dim3(kLongBlock), 0,
+                       c->stream, a, (uint32_t)blocks);
 #endif
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;

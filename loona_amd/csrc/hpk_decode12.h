@@ -828,7 +828,8 @@ __device__ __forceinline__ void seg_stream(const uint2* __restrict__ q, uint32_t
 // kEven: 1 = fills of about equal input size (fewest the window allows), 0 = greedy full windows.
 template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChunk, int kLook, bool kAcc,
           int kCoop = 1, int kSched = 0, int kLongDyn = 1, int kDefer = 1, int kPredSt = 1, int kSpread = 0,
-          int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1, int kSegBig = 15, int kSegSmall = 32>
+          int kSmallFill = 512, uint32_t kLead = 0, int kEven = 1, int kSegBig = 15, int kSegSmall = 32,
+          int kLongK = 0>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -982,6 +983,21 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
     };
     uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
+    // kLongK: long literals left to hpk_decode_long are listed in a.long_list[BA, BB): those of
+    // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
+    auto leave = [&](uint32_t i, uint32_t nb) {
+        if (nb >= a.long_big)
+            a.long_list[BA + atomicAdd(&s_ctr[6], 1u)] = i;
+        else
+            a.long_list[BB - 1u - atomicAdd(&s_ctr[7], 1u)] = i;
+    };
+    if (kLongK) {
+        if (tid == 0) {
+            s_ctr[6] = 0;
+            s_ctr[7] = 0;
+            if (blockIdx.x == 0) a.long_ctr[0] = 0;  // hpk_decode_long's chunk counter (its previous
+        }                                            // launch on this stream has finished)
+    }
 
     uint32_t cur = BA;
     uint32_t gin = 0, gout = 0;  // exact input / output start of the fill (blob-relative + mis)
@@ -990,6 +1006,61 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         gin = a.in_off[cur] + a.in_mis;
         gout = a.out_off[cur] + a.out_mis;
         prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
+    }
+    if (kLongK && cur < BB) {
+        // A range whose first fill's literals hold mostly long-literal bytes (config 3: Zipf lengths)
+        // goes to hpk_decode_long whole: here every fill would stream the long literals' bytes
+        // through the window only to skip them, and wait for its longest short literal. All of the
+        // range's literals are listed (validated: offsets in bounds, regions >= the decoded bound);
+        // any that is not falls back to the fills.
+        const uint32_t cntl = min((uint32_t)kQ, BB - cur);
+        uint32_t lb = 0, tb = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            const uint32_t nb = min(P.io1[r] - P.io0[r], 1u << 20);  // (bad offsets: bounded)
+            tb += t < cntl ? nb : 0u;
+            lb += t < cntl && nb >= a.long_min ? nb : 0u;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            lb += __shfl_xor(lb, d);
+            tb += __shfl_xor(tb, d);
+        }
+        if (tid == 0) {
+            s_ctr[0] = 0;
+            s_ctr[1] = 0;
+            s_ctr[2] = 0;
+        }
+        lds_barrier();
+        if (lane == 0) {
+            atomicAdd(&s_ctr[0], lb);
+            atomicAdd(&s_ctr[1], tb);
+        }
+        lds_barrier();
+        if (s_ctr[0] > s_ctr[1] / 2u) {  // block-uniform
+            bool no = false;
+            for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
+                const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q0 = a.out_off[i], q1 = a.out_off[i + 1];
+                const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
+                                (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
+                if (ok)
+                    leave(i, p1 - p0);
+                else
+                    no = true;
+            }
+            if (__any(no) && lane == 0) s_ctr[2] = 1u;
+            lds_barrier();
+            if (s_ctr[2] == 0) {
+                cur = BB;  // all listed
+            } else {
+                lds_barrier();
+                if (tid == 0) {
+                    s_ctr[6] = 0;
+                    s_ctr[7] = 0;
+                }
+            }
+        }
     }
     if (kMode == 3) t_pre = __builtin_amdgcn_s_memtime() - t_start;
     while (cur < BB) {  // block-uniform
@@ -1034,8 +1105,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 const bool fast = ocap >= (nbytes * 8u) / 5u && (!kAcc || ((o0 | ocap) & 3u) == 0);
                 ex[r] = (p0 - base16) | (nbytes << 16);
                 ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
-                const uint32_t bk = lpt_bucket(nbytes);
-                pos[r] = (bk << 16) | atomicAdd(&s_hist[bk], 1u);
+                if (kLongK && fast && nbytes >= a.long_min) {  // hpk_decode_long's (not queued here)
+                    leave(cur + t, nbytes);
+                } else {
+                    const uint32_t bk = lpt_bucket(nbytes);
+                    pos[r] = (bk << 16) | atomicAdd(&s_hist[bk], 1u);
+                }
             }
             const uint64_t fb = __ballot(fits);
             kw += (uint32_t)__popcll(fb);
@@ -1069,7 +1144,13 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         const uint32_t k = s_ctr[0];
         if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global
-            if (tid == 0) {
+            bool left = false;
+            if (kLongK) {  // (unless it is hpk_decode_long's)
+                const uint32_t nb = a.in_off[cur + 1] - a.in_off[cur];
+                left = nb >= a.long_min && a.out_off[cur + 1] - a.out_off[cur] >= (nb * 8u) / 5u;
+                if (left && tid == 0) leave(cur, nb);
+            }
+            if (tid == 0 && !left) {
                 const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), last16 * 4 + 3};
                 uint8_t* dst = a.out_base + gout;
                 Lit L = {};
@@ -1111,6 +1192,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
         lds_barrier();
+        // queue entries: the fill's literals less those left to hpk_decode_long (kLongK)
+        const uint32_t kq = kLongK ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(s_bbase[63] + s_hist[63])) : k;
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (pos[r] != 0xFFFFFFFFu) s_q[s_bbase[pos[r] >> 16] + (pos[r] & 0xFFFFu)] = make_uint2(ex[r], ey[r]);
@@ -1147,7 +1230,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             if (cur == BA) t_B0 = td0 - tb0;
         }
         if (kMode == 1) {  // diagnostic: no decode; lengths from the queue keep the fill live
-            for (uint32_t tt = tid; tt < k; tt += G::kBlock) {
+            for (uint32_t tt = tid; tt < kq; tt += G::kBlock) {
                 const uint2 e = s_q[tt];
                 s_lenst[e.y & 0xFFFu] = (e.x >> 16) + s_in[e.x & 0xFFFFu];
             }
@@ -1189,7 +1272,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
             if (kMode == 3) t_long += __builtin_amdgcn_s_memtime() - td0;
         };
-        const uint32_t kl = k - nlong;  // lane-queue entries s_q[nlong, k)
+        const uint32_t kl = kq - nlong;  // lane-queue entries s_q[nlong, kq)
         auto lane_phase = [&](auto dtag) {
             constexpr bool D = decltype(dtag)::value;  // issue write-back slots from the loop
             if (kMode != 1 && kl && kSched == 0) {
@@ -1333,7 +1416,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         // literals whose output region is below the decoded bound (or not dword-aligned for the
         // dword stores): byte stores into the image with a capacity check per byte
-        for (uint32_t tt = tid; kMode != 1 && tt < k; tt += G::kBlock) {
+        for (uint32_t tt = tid; kMode != 1 && tt < kq; tt += G::kBlock) {
             const uint2 e = s_q[tt];
             if (e.y & kQ7Byte) {
                 const uint32_t i = e.y & 0xFFFu;
@@ -1353,6 +1436,14 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     if (pk) {
         lds_barrier();
         flush(pcur, pk, pG0, pG1);
+    }
+    if (kLongK) {  // how many literals this workgroup left to hpk_decode_long (0 included: the
+                   // counts are reused across calls)
+        lds_barrier();
+        if (tid == 0) {
+            a.long_wg[blockIdx.x] = s_ctr[6];
+            a.long_wg[256 + blockIdx.x] = s_ctr[7];
+        }
     }
     if (kMode == 3 && lane == 0) {
         const uint64_t gwi = (uint64_t)blockIdx.x * kWaves + (tid >> 6);

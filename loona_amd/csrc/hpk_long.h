@@ -1,0 +1,317 @@
+// hpk_long.h — long-literal decode kernel (v19): one lane per literal, streaming from HBM.
+//
+// The fill kernel (hpk_decode12 with kLongK) leaves the literals of >= long_min encoded bytes whose
+// region holds the decoded bound to this kernel, launched right after it on the same stream: fill
+// workgroup g lists them in long_list[its literal range), those of >= long_big bytes from the front
+// (long_wg[g] of them) and the others from the back (long_wg[256 + g]). Measured on config 3
+// (profiles/r02/rejected/), a cooperative walk costs 0.47-0.9 VALU per input bit and wave
+// (speculative segments resync slowly on header text: 78 % within 64 bits) against ~0.08 for a lane
+// walk, and a fill of the fill kernel waits for its longest literal, decoded by one lane. So here a
+// literal is decoded by ONE lane with the fill kernel's two-lookup step, and the parallelism comes
+// from decoding tens of thousands of long literals at once:
+//   * one workgroup per CU, no fills and no barriers in the loop: a lane that finishes takes the
+//     next long literal from its wave's LDS queue; a wave whose queue runs dry claims the next 64
+//     entries of the lists (one device-scope atomic), all of the >= long_big class first (a rough
+//     longest-first order: the longest literals start first, the short ones fill in);
+//   * each lane streams its literal through an input ring in LDS (dword j of lane t at
+//     ring[j % kRing][t]: conflict-free). Global loads are issued only at wave-uniform refill points,
+//     every kU steps, two 16-byte chunks per lane into registers, and written to the ring at the
+//     NEXT refill point: a load has kU steps to land before anything waits on it (a load waited for
+//     where a lane needs it stalls the whole wave for the HBM latency at every 16 bytes);
+//   * decoded bytes go to a 64-byte output ring per lane in LDS (unconditional byte stores, a
+//     lane's dummy byte for the slots a step does not fill, as the fill kernel's kPred) and leave it
+//     at refill points as 16-byte stores of whole 16-byte groups of the output (a literal's first
+//     and last group bytewise): scattered dword stores straight from the step cost a TA cycle per
+//     lane and dword (0.8 ms of config 3 in the first measurement);
+//   * a literal that ends is finished (padding check, last bytes, length, status) at the next
+//     refill point, outside the steps.
+// Semantics are the fill kernel's lane walk (huffman.rs:95-161): the walk stops where no code fits,
+// an EOS is EOSInString at once, then >7 residual bits PaddingTooLarge, non-ones InvalidPadding.
+#pragma once
+#include "hpk_decode12.h"
+
+namespace hpkdec {
+
+__device__ __forceinline__ uint4 gload16(const DecodeArgs& a, uint32_t q, uint32_t last16) {
+    return reinterpret_cast<const uint4*>(a.in_base)[min(q, last16)];
+}
+
+// kBlock threads (one workgroup per CU), kU steps between refill points, kRing input dwords and
+// 64 output bytes per lane. kDiag (diagnostic builds): per-wave counters into a.dbg[wave * 16 + i]
+// (scripts/diag_decode.py).
+template <int kBlock, int kU, int kRing, int kDiag = 0>
+__global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t fill_grid) {
+    constexpr int kWaves = kBlock / 64;
+    constexpr uint32_t kChunk = 64;            // list entries per claim (one per lane)
+    constexpr uint32_t kQ = 2 * kChunk;        // per-wave queue: < 64 left + one claim
+    constexpr uint32_t kOB = 64;               // output ring bytes per lane
+    constexpr uint32_t kOS = kOB + 4;          // its stride (17 dwords: conflict-free), dummy at kOB
+    static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
+    static_assert(kBlock >= 256, "one thread per fill workgroup (<= 256 of them)");
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[HPK_LUT_SIZE];
+    __shared__ __attribute__((aligned(16))) uint16_t s_lo[HPK_LO_SIZE];
+    __shared__ uint32_t s_ring[kRing * kBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[kOS * kBlock];
+    __shared__ uint32_t s_q[kWaves][kQ];       // per wave: long literals claimed, not started
+    __shared__ uint32_t s_b1[257], s_b2[257];  // exclusive prefix of the two classes' counts
+    __shared__ uint32_t s_w1[kWaves], s_w2[kWaves];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    {  // class counts per fill workgroup (one thread each), scanned
+        const uint32_t g = tid;
+        const uint32_t c1 = g < fill_grid ? a.long_wg[g] : 0u, c2 = g < fill_grid ? a.long_wg[256 + g] : 0u;
+        uint32_t x1 = c1, x2 = c2;  // inclusive scans within the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y1 = __shfl_up(x1, d), y2 = __shfl_up(x2, d);
+            if (lane >= (uint32_t)d) {
+                x1 += y1;
+                x2 += y2;
+            }
+        }
+        if (lane == 63) {
+            s_w1[wv] = x1;
+            s_w2[wv] = x2;
+        }
+        __syncthreads();
+        for (uint32_t w = 0; w < wv; ++w) {
+            x1 += s_w1[w];
+            x2 += s_w2[w];
+        }
+        if (g < fill_grid) {  // s_b[g] = exclusive prefix; s_b[fill_grid] = the total
+            s_b1[g] = x1 - c1;
+            s_b2[g] = x2 - c2;
+        }
+        if (g == fill_grid - 1u) {
+            s_b1[fill_grid] = x1;
+            s_b2[fill_grid] = x2;
+        }
+    }
+    __syncthreads();
+    const uint32_t total1 = s_b1[fill_grid], total2 = s_b2[fill_grid];
+    if (total1 + total2 == 0) return;  // nothing left to this kernel (config 2 / 5)
+    for (uint32_t t = tid; t < HPK_LUT_SIZE / 4; t += kBlock)
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut2)[t];
+    for (uint32_t t = tid; t < (uint32_t)HPK_LO_SIZE * 2 / 16; t += kBlock)
+        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+    __syncthreads();
+    const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
+    const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;
+    const uint32_t nch1 = (total1 + kChunk - 1) / kChunk, nch = nch1 + (total2 + kChunk - 1) / kChunk;
+    uint32_t* ring = s_ring + tid;        // input dword j: ring[(j % kRing) * kBlock]
+    uint8_t* ob8 = s_out + tid * kOS;     // output byte p: ob8[p % kOB]
+    uint8_t* const dmy = ob8 + kOB;
+    bool more = true;               // wave-uniform: claims may remain
+    uint32_t qh = 0, qt = 0;        // wave-uniform: the wave's queue s_q[wv][qh, qt) (mod kQ)
+    // Lane state. Input positions are relative to the literal's first 16-byte chunk q0: X = bit
+    // position + 31 (the fill kernel's convention), the pair (d0, d1) = dwords (X >> 5) - 1 and
+    // X >> 5, d2 the next; the ring holds dwords [.., h) (h a multiple of 8), the registers P the next
+    // 8. Output positions are byte addresses relative to out_base: o0 the literal's first, ob the
+    // next, fl the first not yet stored to global memory.
+    bool act = false, live = false, pend = false, done = false;
+    uint32_t idx = 0, X = 0, Eb = 0, d0 = 0, d1 = 0, d2 = 0, st = HPK_OK, q0 = 0, span = 0, h = 0;
+    uint32_t o0 = 0, ob = 0, fl = 0;
+    uint4 P0 = {}, P1 = {};
+    unsigned long long dg[10] = {};  // kDiag: 0 cycles, 1 points, 2 lane-steps, 3 stalled, 4 idle,
+                                     // 5 assign cycles, 6 step cycles, 7 refill cycles, 8 literals
+    const unsigned long long dt0 = kDiag ? __builtin_amdgcn_s_memtime() : 0;
+    for (;;) {
+        unsigned long long dtp = kDiag ? __builtin_amdgcn_s_memtime() : 0;
+        if (kDiag) dg[1] += 1;
+        // ---- refill point (wave-uniform) ----
+        // 1. the chunks loaded at the previous point go to the ring
+        if (pend) {
+            const uint32_t b = h & (kRing - 1u);
+            ring[(b + 0) * kBlock] = __builtin_bswap32(P0.x);
+            ring[(b + 1) * kBlock] = __builtin_bswap32(P0.y);
+            ring[(b + 2) * kBlock] = __builtin_bswap32(P0.z);
+            ring[(b + 3) * kBlock] = __builtin_bswap32(P0.w);
+            ring[(b + 4) * kBlock] = __builtin_bswap32(P1.x);
+            ring[(b + 5) * kBlock] = __builtin_bswap32(P1.y);
+            ring[(b + 6) * kBlock] = __builtin_bswap32(P1.z);
+            ring[(b + 7) * kBlock] = __builtin_bswap32(P1.w);
+            h += 8u;
+            pend = false;
+        }
+        // 2. a literal whose first chunks just arrived: its window
+        if (act && !live && (h != 0 || span == 0)) {
+            const uint32_t j = X >> 5;  // 0..4
+            d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];  // (unread when j == 0: X is dword-aligned)
+            d1 = ring[j * kBlock];
+            d2 = ring[(j + 1u) * kBlock];
+            live = true;
+        }
+        // 3. whole 16-byte groups of output to global memory (a literal's first one bytewise)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t gb = fl & ~15u;
+            if (act && gb + 16u <= ob) {
+                if (fl == gb) {
+                    const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + (gb & (kOB - 1u)));
+                    *reinterpret_cast<uint4*>(a.out_base + gb) = make_uint4(s[0], s[1], s[2], s[3]);
+                } else {
+                    for (uint32_t p = fl; p < gb + 16u; ++p) a.out_base[p] = ob8[p & (kOB - 1u)];
+                }
+                fl = gb + 16u;
+            }
+        }
+        // 4. a literal that ended in the last steps: padding check, last bytes, length, status
+        if (done) {
+            if (st == HPK_OK) st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
+            for (uint32_t p = fl; p < ob; ++p) a.out_base[p] = ob8[p & (kOB - 1u)];
+            a.out_len[idx] = ob - o0;
+            a.status[idx] = (uint8_t)st;
+            act = false;
+            live = false;
+            done = false;
+        }
+        if (kDiag) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            dg[7] += t - dtp;
+            dtp = t;
+        }
+        // 5. idle lanes take literals from the wave's queue; when it is dry, claim 64 more list entries
+#pragma unroll 1
+        for (int claims = 0;; ++claims) {
+            const bool want = !act;
+            if (!__any(want)) break;
+            const uint64_t wm = __ballot(want);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
+            if (want && qh + rank < qt) {
+                idx = s_q[wv][(qh + rank) % kQ];
+                act = true;
+                live = false;
+                const uint32_t p0 = a.in_off[idx] + a.in_mis, p1 = a.in_off[idx + 1] + a.in_mis;
+                q0 = p0 >> 4;
+                span = p1 - (q0 << 4);  // bytes from the first chunk's start to the literal's end
+                X = (p0 & 15u) * 8u + 31u;
+                Eb = X + (p1 - p0) * 8u;
+                h = 0;
+                st = HPK_OK;
+                o0 = a.out_off[idx] + a.out_mis;
+                ob = o0;
+                fl = o0;
+            }
+            const uint32_t need = (uint32_t)__popcll(wm);
+            const bool enough = need <= qt - qh;
+            qh += min(need, qt - qh);
+            if (enough || !more || claims == 2) break;  // (at most two claims per refill point)
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(&a.long_ctr[0], 1u);
+            c = (uint32_t)__builtin_amdgcn_readlane((int)c, 0);
+            if (c >= nch) {
+                more = false;
+                break;
+            }
+            const bool big = c < nch1;  // wave-uniform
+            const uint32_t v = (big ? c : c - nch1) * kChunk + lane;
+            const uint32_t* sb = big ? s_b1 : s_b2;
+            const bool ok = v < (big ? total1 : total2);
+            uint32_t li = 0;
+            if (ok) {
+                uint32_t r = 0, hi = fill_grid - 1u;  // the last fill workgroup with sb[r] <= v
+                while (r < hi) {
+                    const uint32_t mid = (r + hi + 1u) >> 1;
+                    if (sb[mid] <= v)
+                        r = mid;
+                    else
+                        hi = mid - 1u;
+                }
+                const uint32_t e = v - sb[r];
+                const uint32_t ba = (uint32_t)((uint64_t)a.n * r / fill_grid);
+                const uint32_t bb = (uint32_t)((uint64_t)a.n * (r + 1u) / fill_grid);
+                li = a.long_list[big ? ba + e : bb - 1u - e];
+            }
+            const uint64_t lm = __ballot(ok);
+            const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+            if (ok) s_q[wv][(qt + lr) % kQ] = li;
+            qt += (uint32_t)__popcll(lm);
+        }
+        if (kDiag) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            dg[5] += t - dtp;
+            dtp = t;
+        }
+        if (!__any(act)) break;  // no literal left for this wave
+        // 6. the next two chunks, while the ring has room for them past the window's first dword
+        if (act && h * 4u < span && h + 8u + 1u <= kRing + (X >> 5)) {
+            P0 = gload16(a, q0 + (h >> 2), last16);
+            P1 = gload16(a, q0 + (h >> 2) + 1u, last16);
+            pend = true;
+        }
+        // ---- kU steps while the input ring holds what a step can reach and the output ring has room ----
+        for (int s = 0; s < kU; ++s) {
+            const bool go = act && live && !done && ((X >> 5) + 4u <= h || h * 4u >= span) && ob - fl <= kOB - 5u;
+            if (kDiag) {
+                dg[2] += (unsigned long long)__popcll(__ballot(go));
+                dg[3] += (unsigned long long)__popcll(__ballot(act && live && !done && !go));
+                dg[4] += (unsigned long long)__popcll(__ballot(!(act && live && !done)));
+            }
+            if (!go) continue;
+            const uint32_t d3 = ring[(((X >> 5) + 2u) & (kRing - 1u)) * kBlock];
+            const uint32_t w = __builtin_amdgcn_alignbit(d0, d1, ~X);
+            const uint32_t rem = Eb - X;
+            const uint32_t e1 = s_lut[w >> (32 - HPK_LUT_BITS)];
+            bool a1, a2;
+            const uint32_t u1 = lut12(e1, rem, a1, a2);
+            bool park = (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);
+            const bool cont = a1 & (a2 | (e1 < HPK_LUT2_TWO));
+            const uint32_t w2 = w << u1;
+            const uint32_t rem2 = rem - u1;
+            const uint32_t e2 = s_lut[w2 >> (32 - HPK_LUT_BITS)];
+            bool b1, b2;
+            const uint32_t u2 = lut12(e2, rem2, b1, b2);
+            b1 &= cont;
+            b2 &= cont;
+            *(a1 ? ob8 + (ob & (kOB - 1u)) : dmy) = (uint8_t)e1;
+            *(a2 ? ob8 + ((ob + 1u) & (kOB - 1u)) : dmy) = (uint8_t)(e1 >> 16);
+            ob += (uint32_t)a1 + (uint32_t)a2;
+            *(b1 ? ob8 + (ob & (kOB - 1u)) : dmy) = (uint8_t)e2;
+            *(b2 ? ob8 + ((ob + 1u) & (kOB - 1u)) : dmy) = (uint8_t)(e2 >> 16);
+            ob += (uint32_t)b1 + (uint32_t)b2;
+            park |= cont & (e2 < HPK_LUT2_ONE) & (rem2 > (uint32_t)HPK_LUT_BITS);
+            const uint32_t xn = X + u1 + (cont ? u2 : 0u);
+            const bool cross = (xn ^ X) > 31u;
+            d0 = cross ? d1 : d0;
+            d1 = cross ? d2 : d1;
+            d2 = cross ? d3 : d2;
+            X = xn;
+            bool prog = a1 | park;
+            if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup
+                const uint32_t wp = __builtin_amdgcn_alignbit(d0, d1, ~X);
+                uint32_t sy, len;
+                bool eos;
+                lo_decode(wp, s_lo, sy, len, eos);
+                if (len > Eb - X) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+                    st = HPK_PADDING_TOO_LARGE;
+                    prog = false;
+                } else if (eos) {  // huffman.rs:112-116
+                    st = HPK_EOS_IN_STRING;
+                    prog = false;
+                } else {
+                    ob8[ob & (kOB - 1u)] = (uint8_t)sy;
+                    ob += 1u;
+                    X += len;
+                    const uint32_t j = X >> 5;
+                    d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];
+                    d1 = ring[(j & (kRing - 1u)) * kBlock];
+                    d2 = ring[((j + 1u) & (kRing - 1u)) * kBlock];
+                }
+            }
+            done = !prog;  // the literal has ended: finished at the next refill point
+            if (kDiag) dg[8] += (unsigned long long)__popcll(__ballot(done));
+        }
+        if (kDiag) dg[6] += __builtin_amdgcn_s_memtime() - dtp;
+    }
+    if (kDiag) {
+        dg[0] = __builtin_amdgcn_s_memtime() - dt0;
+        const uint32_t gw = blockIdx.x * (uint32_t)kWaves + wv;
+        if (lane < 10) {
+            unsigned long long v = 0;
+#pragma unroll
+            for (int i = 0; i < 10; ++i) v = lane == (uint32_t)i ? dg[i] : v;
+            a.dbg[gw * 16u + lane] = v;
+        }
+    }
+}
+
+}  // namespace hpkdec

@@ -40,7 +40,7 @@ with torch.cuda.stream(s):
     s.synchronize()
     us = e0.elapsed_time(e1) / K * 1e3
 res = {"config": w.name, "mode": mode, "us_per_launch": round(us, 2)}
-if mode in (0, 2, 3, 4):
+if mode in (0, 2, 3, 4, 5):
     ok = bool((st.cpu().numpy() == 0).all()) and np.array_equal(ol.cpu().numpy(), np.diff(w.dec_off.astype(np.int64)))
     res["lengths_ok"] = ok
 if mode == 4:
@@ -59,4 +59,13 @@ if mode == 3:
              "setupB_fill0", "byte_pass", "last_flush"]
     res["stamps_per_wave"] = {nm: {"mean": round(float(st8[:, i].mean()), 1), "max": int(st8[:, i].max())}
                               for i, nm in enumerate(names)}
+if mode == 5:  # hpk_decode_long's per-wave counters
+    L = _lib.lib()
+    L.hpk_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    buf = np.zeros(256 * 16 * 16, np.uint64)
+    got = L.hpk_debug_stamps(buf.ctypes.data, buf.size)
+    st8 = buf[:got].reshape(-1, 16).astype(np.int64)
+    names = ["cycles", "points", "lane_steps", "stalled", "idle", "assign_cyc", "step_cyc", "ringwrite_cyc", "literals"]
+    res["long_per_wave"] = {nm: {"mean": round(float(st8[:, i].mean()), 1), "max": int(st8[:, i].max()),
+                                 "min": int(st8[:, i].min())} for i, nm in enumerate(names)}
 print(json.dumps(res), flush=True)
