@@ -43,8 +43,14 @@ using namespace hpkdec;
 constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2, kChunk = 64, kLook = 2, kSched = 1;
 constexpr bool kAcc = false;
 constexpr int kCoop = 0;  // (v16: literals of >= 224 encoded bytes one wave each; v19: hpk_decode_long)
-constexpr int kLongK = 1;  // long literals left to hpk_decode_long
-constexpr int kSpread = 1;  // lane-queue slots interleaved over the waves (fills of few literals use every SIMD)
+#ifndef HPK_LONGK
+#define HPK_LONGK 1
+#endif
+#ifndef HPK_SPREAD
+#define HPK_SPREAD 0
+#endif
+constexpr int kLongK = HPK_LONGK;  // long literals left to hpk_decode_long
+constexpr int kSpread = HPK_SPREAD;  // lane-queue slots interleaved over the waves (fills of few literals use every SIMD)
 #ifndef HPK_LONG_MIN
 #define HPK_LONG_MIN 64  // encoded bytes: literals from here on go to hpk_decode_long
 #endif
@@ -199,8 +205,9 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
         default: LONG_LAUNCH(kLongBlock, kLongU, kLongRing);
     }
 #else
-    hipLaunchKernelGGL((hpk_decode_long<kLongBlock, kLongU, kLongRing>), dim3((uint32_t)c->num_cu), dim3(kLongBlock), 0,
-                       c->stream, a, (uint32_t)blocks);
+    if (kLongK)
+        hipLaunchKernelGGL((hpk_decode_long<kLongBlock, kLongU, kLongRing>), dim3((uint32_t)c->num_cu), dim3(kLongBlock), 0,
+                           c->stream, a, (uint32_t)blocks);
 #endif
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;

@@ -32,9 +32,34 @@
 
 namespace hpkdec {
 
-__device__ __forceinline__ uint4 gload16(const DecodeArgs& a, uint32_t q, uint32_t last16) {
-    return reinterpret_cast<const uint4*>(a.in_base)[min(q, last16)];
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Raw buffer resources (gfx9 dword 3): accesses past num_records bytes are dropped (stores) or read 0
+// (loads), and every access is ONE VGPR offset plus its data registers, which the kernel keeps live
+// (pin) so that no later instruction overwrites a register a pending store still reads.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
+
+// Bytes [lo, hi) of the 16-byte output group at byte offset gb (v: its four dwords, b[e] = byte e in
+// the low byte): whole dwords by dword stores, the rest bytewise (straight-line, no loop).
+__device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t gb, uint32_t lo, uint32_t hi,
+                                           const uint32_t (&v)[4], const uint32_t (&b)[16]) {
+#pragma unroll
+    for (uint32_t d = 0; d < 4u; ++d) {
+        if (lo <= 4u * d && 4u * d + 4u <= hi) {
+            __builtin_amdgcn_raw_buffer_store_b32(v[d], r, gb, 4 * d, 0);
+        } else {
+#pragma unroll
+            for (uint32_t e = 0; e < 4u; ++e)
+                if (4u * d + e >= lo && 4u * d + e < hi)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b[4u * d + e], r, gb, 4 * d + e, 0);
+        }
+    }
+}
+
+// Keep a value's register live (and unchanged) up to here.
+__device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 
 // kBlock threads (one workgroup per CU), kU steps between refill points, kRing input dwords and
 // 64 output bytes per lane. kDiag (diagnostic builds): per-wave counters into a.dbg[wave * 16 + i]
@@ -52,7 +77,7 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
     __shared__ __attribute__((aligned(16))) uint16_t s_lo[HPK_LO_SIZE];
     __shared__ uint32_t s_ring[kRing * kBlock];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[kOS * kBlock];
-    __shared__ uint32_t s_q[kWaves][kQ];       // per wave: long literals claimed, not started
+    __shared__ uint4 s_q[kWaves][kQ];          // per wave: literals claimed, not started (index, offsets)
     __shared__ uint32_t s_b1[257], s_b2[257];  // exclusive prefix of the two classes' counts
     __shared__ uint32_t s_w1[kWaves], s_w2[kWaves];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -95,7 +120,11 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
     __syncthreads();
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
-    const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;
+    // (whole 16-byte chunks: a load that reaches past num_records reads 0 in all its dwords)
+    const __amdgpu_buffer_rsrc_t r_in = buf_rsrc(a.in_base, (in_end + 15u) & ~15u);
+    const __amdgpu_buffer_rsrc_t r_out = buf_rsrc(a.out_base, a.out_cap + a.out_mis);
+    const __amdgpu_buffer_rsrc_t r_len = buf_rsrc(a.out_len, min(a.n, 0x3FFFFFFFu) * 4u);
+    const __amdgpu_buffer_rsrc_t r_st = buf_rsrc(a.status, a.n);
     const uint32_t nch1 = (total1 + kChunk - 1) / kChunk, nch = nch1 + (total2 + kChunk - 1) / kChunk;
     uint32_t* ring = s_ring + tid;        // input dword j: ring[(j % kRing) * kBlock]
     uint8_t* ob8 = s_out + tid * kOS;     // output byte p: ob8[p % kOB]
@@ -110,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
     bool act = false, live = false, pend = false, done = false;
     uint32_t idx = 0, X = 0, Eb = 0, d0 = 0, d1 = 0, d2 = 0, st = HPK_OK, q0 = 0, span = 0, h = 0;
     uint32_t o0 = 0, ob = 0, fl = 0;
-    uint4 P0 = {}, P1 = {};
+    u32x4 P0 = {}, P1 = {};
     unsigned long long dg[10] = {};  // kDiag: 0 cycles, 1 points, 2 lane-steps, 3 stalled, 4 idle,
                                      // 5 assign cycles, 6 step cycles, 7 refill cycles, 8 literals
     const unsigned long long dt0 = kDiag ? __builtin_amdgcn_s_memtime() : 0;
@@ -140,26 +169,63 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
             d2 = ring[(j + 1u) * kBlock];
             live = true;
         }
-        // 3. whole 16-byte groups of output to global memory (a literal's first one bytewise)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        // 3. output to global memory: a literal's first 16-byte group (it shares it with the previous
+        // region) once complete, bytewise; then whole groups as 16-byte stores. Every register a store
+        // reads its data from stays live until after the steps (pin): the compiler reuses a store's
+        // data register only after waiting for the store to complete, which would stall the first
+        // step of every period on a store round trip.
+        u32x4 gv[4];
+        uint32_t hv[4], hb[16], tv[4], tb[16], lv = 0, sv = 0;
+        uint32_t ha = 0, ga = 0, ta = 0, ia = 0, ja = 0;  // their addresses (pinned too)
+        {
             const uint32_t gb = fl & ~15u;
-            if (act && gb + 16u <= ob) {
-                if (fl == gb) {
-                    const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + (gb & (kOB - 1u)));
-                    *reinterpret_cast<uint4*>(a.out_base + gb) = make_uint4(s[0], s[1], s[2], s[3]);
-                } else {
-                    for (uint32_t p = fl; p < gb + 16u; ++p) a.out_base[p] = ob8[p & (kOB - 1u)];
-                }
+            ha = gb;
+            if (act && fl != gb && gb + 16u <= ob) {
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + (gb & (kOB - 1u)));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hv[e] = s[e];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) hb[e] = hv[e >> 2] >> (8 * (e & 3));
+                store_part(r_out, gb, fl - gb, 16u, hv, hb);
                 fl = gb + 16u;
             }
+        }
+        {  // (fl is group-aligned here.) All four groups are read before any is stored.
+            ga = fl;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + ((fl + 16u * k) & (kOB - 1u)));
+                gv[k] = u32x4{s[0], s[1], s[2], s[3]};
+            }
+            uint32_t ng = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (act && ga + 16u * (k + 1) <= ob) {
+                    __builtin_amdgcn_raw_buffer_store_b128(gv[k], r_out, ga, 16 * k, 0);
+                    ng = k + 1;
+                }
+            }
+            fl += 16u * ng;
         }
         // 4. a literal that ended in the last steps: padding check, last bytes, length, status
         if (done) {
             if (st == HPK_OK) st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
-            for (uint32_t p = fl; p < ob; ++p) a.out_base[p] = ob8[p & (kOB - 1u)];
-            a.out_len[idx] = ob - o0;
-            a.status[idx] = (uint8_t)st;
+            if (ob > fl) {  // [fl, ob) lies in one group
+                const uint32_t gb = fl & ~15u;
+                ta = gb;
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + (gb & (kOB - 1u)));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) tv[e] = s[e];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) tb[e] = tv[e >> 2] >> (8 * (e & 3));
+                store_part(r_out, gb, fl - gb, ob - gb, tv, tb);
+            }
+            lv = ob - o0;
+            sv = st;
+            ia = idx * 4u;
+            ja = idx;
+            __builtin_amdgcn_raw_buffer_store_b32(lv, r_len, ia, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sv, r_st, ja, 0, 0);
             act = false;
             live = false;
             done = false;
@@ -177,17 +243,18 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
             const uint64_t wm = __ballot(want);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
             if (want && qh + rank < qt) {
-                idx = s_q[wv][(qh + rank) % kQ];
+                const uint4 e = s_q[wv][(qh + rank) % kQ];
+                idx = e.x;
                 act = true;
                 live = false;
-                const uint32_t p0 = a.in_off[idx] + a.in_mis, p1 = a.in_off[idx + 1] + a.in_mis;
+                const uint32_t p0 = e.y + a.in_mis, p1 = e.z + a.in_mis;
                 q0 = p0 >> 4;
                 span = p1 - (q0 << 4);  // bytes from the first chunk's start to the literal's end
                 X = (p0 & 15u) * 8u + 31u;
                 Eb = X + (p1 - p0) * 8u;
                 h = 0;
                 st = HPK_OK;
-                o0 = a.out_off[idx] + a.out_mis;
+                o0 = e.w + a.out_mis;
                 ob = o0;
                 fl = o0;
             }
@@ -206,21 +273,25 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
             const uint32_t v = (big ? c : c - nch1) * kChunk + lane;
             const uint32_t* sb = big ? s_b1 : s_b2;
             const bool ok = v < (big ? total1 : total2);
-            uint32_t li = 0;
-            if (ok) {
-                uint32_t r = 0, hi = fill_grid - 1u;  // the last fill workgroup with sb[r] <= v
-                while (r < hi) {
-                    const uint32_t mid = (r + hi + 1u) >> 1;
-                    if (sb[mid] <= v)
-                        r = mid;
-                    else
-                        hi = mid - 1u;
-                }
-                const uint32_t e = v - sb[r];
-                const uint32_t ba = (uint32_t)((uint64_t)a.n * r / fill_grid);
-                const uint32_t bb = (uint32_t)((uint64_t)a.n * (r + 1u) / fill_grid);
-                li = a.long_list[big ? ba + e : bb - 1u - e];
+            // straight-line (no branch around the loads): a load under a branch leaves the compiler
+            // unsure whether its register is still pending, and it then waits for all memory
+            // operations (the refill loads included) before the steps reuse the register
+            const uint32_t vv = ok ? v : 0u;
+            uint32_t r = 0, hi = fill_grid - 1u;  // the last fill workgroup with sb[r] <= vv
+            while (r < hi) {
+                const uint32_t mid = (r + hi + 1u) >> 1;
+                if (sb[mid] <= vv)
+                    r = mid;
+                else
+                    hi = mid - 1u;
             }
+            const uint32_t e = vv - sb[r];
+            const uint32_t ba = (uint32_t)((uint64_t)a.n * r / fill_grid);
+            const uint32_t bb = (uint32_t)((uint64_t)a.n * (r + 1u) / fill_grid);
+            const uint32_t lpos = ok ? (big ? ba + e : bb - 1u - e) : 0u;
+            const uint32_t i0 = a.long_list[lpos];  // (entry 0 when !ok: a load either way)
+            const uint32_t i = ok ? i0 : 0u;
+            const uint4 li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.out_off[i]);
             const uint64_t lm = __ballot(ok);
             const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
             if (ok) s_q[wv][(qt + lr) % kQ] = li;
@@ -234,8 +305,8 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
         if (!__any(act)) break;  // no literal left for this wave
         // 6. the next two chunks, while the ring has room for them past the window's first dword
         if (act && h * 4u < span && h + 8u + 1u <= kRing + (X >> 5)) {
-            P0 = gload16(a, q0 + (h >> 2), last16);
-            P1 = gload16(a, q0 + (h >> 2) + 1u, last16);
+            P0 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u, 0, 0);
+            P1 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u + 16u, 0, 0);
             pend = true;
         }
         // ---- kU steps while the input ring holds what a step can reach and the output ring has room ----
@@ -301,6 +372,27 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
             if (kDiag) dg[8] += (unsigned long long)__popcll(__ballot(done));
         }
         if (kDiag) dg[6] += __builtin_amdgcn_s_memtime() - dtp;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pin(gv[k].x);
+            pin(gv[k].y);
+            pin(gv[k].z);
+            pin(gv[k].w);
+            pin(hv[k]);
+            pin(tv[k]);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            pin(hb[e]);
+            pin(tb[e]);
+        }
+        pin(lv);
+        pin(sv);
+        pin(ha);
+        pin(ga);
+        pin(ta);
+        pin(ia);
+        pin(ja);
     }
     if (kDiag) {
         dg[0] = __builtin_amdgcn_s_memtime() - dt0;
