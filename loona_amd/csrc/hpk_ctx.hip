@@ -74,21 +74,18 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     return c;
 }
 
-int hpk_long_state(hpk_ctx* c, uint32_t n, uint32_t** state, uint32_t** list) {
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list) {
     int j = -1;
     for (int k = 0; k < hpk_ctx::kLongSlots; ++k)
-        if (c->long_buf[k] && c->long_stream[k] == c->stream) j = k;
+        if (c->long_list[k] && c->long_stream[k] == c->stream) j = k;
     if (j < 0) {
         j = 0;
-        while (j < hpk_ctx::kLongSlots && c->long_buf[j]) ++j;
+        while (j < hpk_ctx::kLongSlots && c->long_list[j]) ++j;
         if (j == hpk_ctx::kLongSlots) {  // all taken: reuse the oldest once its stream has drained
             j = c->long_next;
             c->long_next = (j + 1) % hpk_ctx::kLongSlots;
             HIP_TRY(hipStreamSynchronize(c->long_stream[j]));
-        } else {
-            HIP_TRY(hipMalloc(&c->long_buf[j], hpk_ctx::kLongWords * sizeof(uint32_t)));
         }
-        HIP_TRY(hipMemsetAsync(c->long_buf[j], 0, hpk_ctx::kLongWords * sizeof(uint32_t), c->stream));
         c->long_stream[j] = c->stream;
     }
     if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
@@ -100,7 +97,6 @@ int hpk_long_state(hpk_ctx* c, uint32_t n, uint32_t** state, uint32_t** list) {
         HIP_TRY(hipMalloc(&c->long_list[j], cap * sizeof(uint32_t)));
         c->long_list_cap[j] = cap;
     }
-    *state = c->long_buf[j];
     *list = c->long_list[j];
     return HPK_E_OK;
 }
@@ -119,10 +115,8 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
-    for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
-        if (c->long_buf[j]) (void)hipFree(c->long_buf[j]);
+    for (int j = 0; j < hpk_ctx::kLongSlots; ++j)
         if (c->long_list[j]) (void)hipFree(c->long_list[j]);
-    }
     for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
         if (c->ev_in[j]) (void)hipEventDestroy(c->ev_in[j]);
         if (c->ev_run[j]) (void)hipEventDestroy(c->ev_run[j]);

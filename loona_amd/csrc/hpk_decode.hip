@@ -32,7 +32,7 @@
 // A literal too large for the window is decoded by one lane straight from global memory.
 #include <stdlib.h>
 
-#include "hpk_long.h"
+#include "hpk_decode12.h"
 
 using namespace hpkdec;
 
@@ -49,17 +49,14 @@ constexpr int kCoop = 0;  // (v16: literals of >= 224 encoded bytes one wave eac
 #ifndef HPK_SPREAD
 #define HPK_SPREAD 0
 #endif
-constexpr int kLongK = HPK_LONGK;  // long literals left to hpk_decode_long
+constexpr int kLongK = HPK_LONGK;  // long literals left to the long-literal phase (hpk_long.h)
 constexpr int kSpread = HPK_SPREAD;  // lane-queue slots interleaved over the waves (fills of few literals use every SIMD)
 #ifndef HPK_LONG_MIN
-#define HPK_LONG_MIN 64  // encoded bytes: literals from here on go to hpk_decode_long
+#define HPK_LONG_MIN 64  // encoded bytes: literals from here on go to the long-literal phase
 #endif
 #ifndef HPK_LONG_BIG
-#define HPK_LONG_BIG 1024  // hpk_decode_long takes these first (longest-first, roughly)
+#define HPK_LONG_BIG 1024  // the long-literal phase takes these first (longest-first, roughly)
 #endif
-// hpk_decode_long: one 512-thread workgroup per CU (2 waves per SIMD), refill every 8 steps, 32-dword
-// input ring per lane
-constexpr int kLongBlock = 512, kLongU = 8, kLongRing = 32;
 using Geo = Geo12<kWaves, kW, kO, kQ>;
 #ifndef HPK_LONGDYN
 #define HPK_LONGDYN 1
@@ -117,10 +114,8 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
-    uint32_t *ls = nullptr, *ll = nullptr;
-    if (int rc = hpk_long_state(c, b.n, &ls, &ll)) return rc;
-    a.long_wg = ls;
-    a.long_ctr = ls + 512;
+    uint32_t* ll = nullptr;
+    if (int rc = hpk_long_list(c, b.n, &ll)) return rc;
     a.long_list = ll;
     a.long_min = HPK_LONG_MIN;
     a.long_big = HPK_LONG_BIG;
@@ -132,7 +127,6 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
-    if (blocks > 256) blocks = 256;  // (long_wg holds 256 counts)
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
 #ifdef HPK_DIAG
     if (g_debug_mode < 0) {
@@ -160,9 +154,18 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
         case 4:
             hipLaunchKernelGGL(DEC_KERNEL(4), grid, block, 0, c->stream, a);
             break;
-        case 5:  // the product kernel; hpk_decode_long with per-wave counters (below)
-            hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
+        case 5: {  // the product kernel with per-wave counters of the long-literal phase (8 waves)
+            const size_t need = (size_t)blocks * 8 * 16;
+            if (need > g_dbg_n) {
+                (void)hipFree(g_dbg);
+                HIP_TRY(hipMalloc(&g_dbg, need * 8));
+                g_dbg_n = need;
+            }
+            HIP_TRY(hipMemsetAsync(g_dbg, 0, need * 8, c->stream));
+            a.dbg = g_dbg;
+            hipLaunchKernelGGL(DEC_KERNEL(5), grid, block, 0, c->stream, a);
             break;
+        }
         default:
             hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
     }
@@ -170,45 +173,6 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
 #endif
     HIP_TRY(hipGetLastError());
-#ifdef HPK_DIAG
-    // diagnostic variants of hpk_decode_long (HPK_LONG_VAR), with per-wave counters in mode 5
-    static int long_var = -1;
-    if (long_var < 0) {
-        const char* lv = getenv("HPK_LONG_VAR");
-        long_var = lv ? atoi(lv) : 0;
-    }
-    const uint32_t lwaves = long_var == 1 ? 12u : (long_var == 2 ? 4u : 8u);
-    if (g_debug_mode == 5) {
-        const size_t need = (size_t)c->num_cu * lwaves * 16;
-        if (need > g_dbg_n) {
-            (void)hipFree(g_dbg);
-            HIP_TRY(hipMalloc(&g_dbg, need * 8));
-            g_dbg_n = need;
-        }
-        HIP_TRY(hipMemsetAsync(g_dbg, 0, need * 8, c->stream));
-        a.dbg = g_dbg;
-    }
-#define LONG_LAUNCH(B, U, R)                                                                                   \
-    do {                                                                                                        \
-        if (g_debug_mode == 5)                                                                                  \
-            hipLaunchKernelGGL((hpk_decode_long<B, U, R, 1>), dim3((uint32_t)c->num_cu), dim3(B), 0, c->stream, a, \
-                               (uint32_t)blocks);                                                               \
-        else                                                                                                    \
-            hipLaunchKernelGGL((hpk_decode_long<B, U, R, 0>), dim3((uint32_t)c->num_cu), dim3(B), 0, c->stream, a, \
-                               (uint32_t)blocks);                                                               \
-    } while (0)
-    switch (long_var) {
-        case 1: LONG_LAUNCH(768, 8, 16); break;
-        case 2: LONG_LAUNCH(256, 8, 32); break;
-        case 3: LONG_LAUNCH(512, 4, 32); break;
-        case 4: LONG_LAUNCH(512, 16, 32); break;
-        default: LONG_LAUNCH(kLongBlock, kLongU, kLongRing);
-    }
-#else
-    if (kLongK)
-        hipLaunchKernelGGL((hpk_decode_long<kLongBlock, kLongU, kLongRing>), dim3((uint32_t)c->num_cu), dim3(kLongBlock), 0,
-                           c->stream, a, (uint32_t)blocks);
-#endif
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
 }

@@ -33,7 +33,7 @@ namespace hpkdec {
 template <int kWaves, int kW, int kO, int kQ>
 struct Geo12 : Geo7<kWaves, kW, kO, kQ, true> {
     using B = Geo7<kWaves, kW, kO, kQ, true>;
-    static constexpr int kLdsBytes = B::kCtrOff + 32;
+    static constexpr int kLdsBytes = B::kCtrOff + 48;
     static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
 };
 
@@ -803,6 +803,12 @@ __device__ __forceinline__ void seg_stream(const uint2* __restrict__ q, uint32_t
     }
 }
 
+}  // namespace hpkdec
+
+#include "hpk_long.h"  // the long-literal phase (kLongK)
+
+namespace hpkdec {
+
 // ------------------------------------------------------------------------------------------
 
 // kMode: 0 product; diagnostics (never the default): 1 no decode (fill structure only), 2 no
@@ -810,7 +816,7 @@ __device__ __forceinline__ void seg_stream(const uint2* __restrict__ q, uint32_t
 // steps, waiting at the fill-top barrier, before the first fill, fill setup up to the entries,
 // fill setup from there to the decode, in long literals, the first fill's two setup parts, the
 // byte pass, the last write-back),
-// 4 checked stores (g_chk).
+// 4 checked stores (g_chk), 5 product + per-wave counters of the long-literal phase in a.dbg.
 // kCoop: 1 = long literals by whole waves (product), 0 = every literal by one lane (comparison).
 // kSched: 0 = lanes take queue slots dynamically (ballot + per-wave reservations), 1 = static
 // snake: lane i decodes slots i and 2*block-1-i of the longest-first queue, the second one's
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
     };
     uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
-    // kLongK: long literals left to hpk_decode_long are listed in a.long_list[BA, BB): those of
+    // kLongK: long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
     auto leave = [&](uint32_t i, uint32_t nb) {
         if (nb >= a.long_big)
@@ -995,8 +1001,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         if (tid == 0) {
             s_ctr[6] = 0;
             s_ctr[7] = 0;
-            if (blockIdx.x == 0) a.long_ctr[0] = 0;  // hpk_decode_long's chunk counter (its previous
-        }                                            // launch on this stream has finished)
+            s_ctr[8] = 0;
+            s_ctr[9] = 0;
+        }
     }
 
     uint32_t cur = BA;
@@ -1007,62 +1014,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         gout = a.out_off[cur] + a.out_mis;
         prefetch_fill<G::kBlock>(P, a, tid, cur, min(cur + (uint32_t)kQ, BB), gin & ~15u, rlast16);
     }
-    if (kLongK && cur < BB) {
-        // A range whose first fill's literals hold mostly long-literal bytes (config 3: Zipf lengths)
-        // goes to hpk_decode_long whole: here every fill would stream the long literals' bytes
-        // through the window only to skip them, and wait for its longest short literal. All of the
-        // range's literals are listed (validated: offsets in bounds, regions >= the decoded bound);
-        // any that is not falls back to the fills.
-        const uint32_t cntl = min((uint32_t)kQ, BB - cur);
-        uint32_t lb = 0, tb = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t t = tid + (uint32_t)G::kBlock * r;
-            const uint32_t nb = min(P.io1[r] - P.io0[r], 1u << 20);  // (bad offsets: bounded)
-            tb += t < cntl ? nb : 0u;
-            lb += t < cntl && nb >= a.long_min ? nb : 0u;
-        }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            lb += __shfl_xor(lb, d);
-            tb += __shfl_xor(tb, d);
-        }
-        if (tid == 0) {
-            s_ctr[0] = 0;
-            s_ctr[1] = 0;
-            s_ctr[2] = 0;
-        }
-        lds_barrier();
-        if (lane == 0) {
-            atomicAdd(&s_ctr[0], lb);
-            atomicAdd(&s_ctr[1], tb);
-        }
-        lds_barrier();
-        if (s_ctr[0] > s_ctr[1] / 2u) {  // block-uniform
-            bool no = false;
-            for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
-                const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q0 = a.out_off[i], q1 = a.out_off[i + 1];
-                const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
-                                (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
-                if (ok)
-                    leave(i, p1 - p0);
-                else
-                    no = true;
-            }
-            if (__any(no) && lane == 0) s_ctr[2] = 1u;
-            lds_barrier();
-            if (s_ctr[2] == 0) {
-                cur = BB;  // all listed
-            } else {
-                lds_barrier();
-                if (tid == 0) {
-                    s_ctr[6] = 0;
-                    s_ctr[7] = 0;
-                }
-            }
-        }
-    }
     if (kMode == 3) t_pre = __builtin_amdgcn_s_memtime() - t_start;
+    bool dense_tried = false;  // block-uniform (kLongK): the range's first fill was checked
     while (cur < BB) {  // block-uniform
         const uint32_t cntl = min((uint32_t)kQ, BB - cur);
         const uint32_t base16 = gin & ~15u;
@@ -1087,10 +1040,16 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         lds_barrier();
         uint32_t ex[R], ey[R], pos[R];
         uint32_t kw = 0;
+        uint32_t dlb = 0, dtb = 0;  // (kLongK, first fill) long-literal bytes and all bytes of the candidates
         bool bad = false;  // a literal of this fill's range with decreasing offsets or offsets past a capacity
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            if (kLongK && !dense_tried) {
+                const uint32_t nb = min(P.io1[r] - P.io0[r], 1u << 20);  // (bad offsets: bounded)
+                dtb += t < cntl ? nb : 0u;
+                dlb += t < cntl && nb >= a.long_min ? nb : 0u;
+            }
             bad |= t < cntl && !(P.io0[r] <= P.io1[r] && P.io1[r] <= a.in_cap && P.oo0[r] <= P.oo1[r] &&
                                  P.oo1[r] <= a.out_cap);
             const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
@@ -1126,6 +1085,17 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         if (lane == 0 && kw) atomicAdd(&s_ctr[0], kw);
         if (__any(bad) && lane == 0) s_ctr[5] = 1u;
+        if (kLongK && !dense_tried) {
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                dlb += __shfl_xor(dlb, d);
+                dtb += __shfl_xor(dtb, d);
+            }
+            if (lane == 0) {
+                atomicAdd(&s_ctr[8], dlb);
+                atomicAdd(&s_ctr[9], dtb);
+            }
+        }
         lds_barrier();
         if (kMode == 3) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -1141,6 +1111,46 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
             if (tid == 0) *a.err = 1u;
             break;
+        }
+        if (kLongK && !dense_tried) {
+            // A range whose first fill's literals hold mostly long-literal bytes (config 3: Zipf
+            // lengths) goes to the long-literal phase whole: here every fill would stream the long
+            // literals' bytes through the window only to skip them, and wait for its longest short
+            // literal. All of the range's literals are listed (validated: offsets in bounds, regions
+            // >= the decoded bound); if any is not, the range is decoded by fills after all.
+            dense_tried = true;
+            if (s_ctr[8] > s_ctr[9] / 2u) {  // block-uniform
+                lds_barrier();
+                if (tid == 0) {
+                    s_ctr[6] = 0;  // (this fill's entries are listed again below)
+                    s_ctr[7] = 0;
+                    s_ctr[10] = 0;
+                }
+                lds_barrier();
+                bool no = false;
+                for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
+                    const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q0 = a.out_off[i], q1 = a.out_off[i + 1];
+                    const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
+                                    (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
+                    if (ok)
+                        leave(i, p1 - p0);
+                    else
+                        no = true;
+                }
+                if (__any(no) && lane == 0) s_ctr[10] = 1u;
+                lds_barrier();
+                if (s_ctr[10] == 0) {
+                    cur = BB;  // all listed
+                    break;
+                }
+                lds_barrier();
+                if (tid == 0) {
+                    s_ctr[6] = 0;
+                    s_ctr[7] = 0;
+                }
+                continue;  // this fill again, from its setup (its prefetched offsets and window are still
+                           // in the registers)
+            }
         }
         const uint32_t k = s_ctr[0];
         if (k == 0) {  // literal `cur` alone exceeds the window: one lane decodes it from global
@@ -1437,14 +1447,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         lds_barrier();
         flush(pcur, pk, pG0, pG1);
     }
-    if (kLongK) {  // how many literals this workgroup left to hpk_decode_long (0 included: the
-                   // counts are reused across calls)
-        lds_barrier();
-        if (tid == 0) {
-            a.long_wg[blockIdx.x] = s_ctr[6];
-            a.long_wg[256 + blockIdx.x] = s_ctr[7];
-        }
-    }
     if (kMode == 3 && lane == 0) {
         const uint64_t gwi = (uint64_t)blockIdx.x * kWaves + (tid >> 6);
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
@@ -1462,6 +1464,14 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         a.dbg[gwi * 16 + 11] = t_end - t_tail;
         a.dbg[gwi * 16 + 12] = t_rounds;
         a.dbg[gwi * 16 + 13] = n_longs;
+    }
+    if (kLongK) {  // the literals this workgroup left to the long-literal phase
+        lds_barrier();
+        if (tid == 0) s_ctr[5] = 0;  // its claim counter
+        __syncthreads();  // (every thread's list entries and stores are out)
+        long_phase<512, 8, 32, kMode == 5 ? 1 : 0, G::kBlock>(a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5],
+                                                              reinterpret_cast<uint32_t*>(s_out), s_in,
+                                                              reinterpret_cast<uint4*>(s_q), s_lut, s_lo);
     }
 }
 

@@ -32,12 +32,9 @@ struct DecodeArgs {
     unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
     uint32_t in_cap, out_cap;  // blob sizes (clamped to HPK_MAX_OFFSET): larger offsets are bad
     uint32_t* err;             // sticky error flag (host-mapped): set to 1 on bad offsets
-    // kLongK: literals of >= long_min encoded bytes (region >= the decoded bound) are left to
-    // hpk_decode_long. Fill workgroup g lists them in long_list[its range): those of >= long_big
-    // bytes from the front (long_wg[g] of them), the others from the back (long_wg[256 + g]);
-    // long_ctr[0] = hpk_decode_long's chunk counter (zeroed by the fill kernel)
-    uint32_t* long_wg;
-    uint32_t* long_ctr;
+    // kLongK: literals of >= long_min encoded bytes (region >= the decoded bound) are left to the
+    // long-literal phase (hpk_long.h): fill workgroup g lists them in long_list[its literal range),
+    // those of >= long_big bytes from the front, the others from the back
     uint32_t* long_list;
     uint32_t long_min, long_big;
 };

@@ -37,21 +37,18 @@ struct hpk_ctx {
     // sticky error flag: host-mapped, written (plain store of 1) by a kernel that saw bad offsets
     uint32_t* h_err = nullptr;
     uint32_t* d_err = nullptr;
-    // long-literal kernel state per stream (calls on different streams may overlap): [0, 512) the
-    // fill workgroups' long-literal counts (two classes), [512] hpk_decode_long's chunk counter;
-    // and the list of long literals (one u32 per literal of the batch, grow-only)
+    // the long-literal list per stream (calls on different streams may overlap): one u32 per
+    // literal of the batch, grow-only
     static constexpr int kLongSlots = 8;
-    static constexpr int kLongWords = 520;
     hipStream_t long_stream[kLongSlots] = {};
-    uint32_t* long_buf[kLongSlots] = {};
     uint32_t* long_list[kLongSlots] = {};
     size_t long_list_cap[kLongSlots] = {};
     int long_next = 0;
 };
 
-// The long-literal state for the context's current stream, its list sized for n literals
-// (allocated on first use; HPK_E_OK or an error code).
-int hpk_long_state(hpk_ctx* c, uint32_t n, uint32_t** state, uint32_t** list);
+// The long-literal list for the context's current stream, sized for n literals (allocated on
+// first use; HPK_E_OK or an error code).
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list);
 
 // One batch call as the launchers see it: capacities clamped to HPK_MAX_OFFSET (offsets above
 // them are bad whatever the buffer size).

@@ -1,18 +1,21 @@
-// hpk_long.h — long-literal decode kernel (v19): one lane per literal, streaming from HBM.
+// hpk_long.h — long-literal decode phase (v19): one lane per literal, streaming from HBM.
 //
 // The fill kernel (hpk_decode12 with kLongK) leaves the literals of >= long_min encoded bytes whose
-// region holds the decoded bound to this kernel, launched right after it on the same stream: fill
-// workgroup g lists them in long_list[its literal range), those of >= long_big bytes from the front
-// (long_wg[g] of them) and the others from the back (long_wg[256 + g]). Measured on config 3
+// region holds the decoded bound (and whole ranges dominated by them) to this phase, which runs in
+// the same launch once a workgroup's fills are done (a second launch cost ~4.8 us on batches with
+// nothing to leave). Fill workgroup g lists its literals in long_list[its literal range): those of
+// >= long_big bytes from the front (c1 of them), the others from the back (c2), publishes the
+// counts with a release flag tagged with the call's epoch, and then decodes them, first its own,
+// then any other workgroup's that has published (claims of 64 entries on a per-workgroup device
+// counter; a workgroup whose list is not published yet decodes its own). Measured on config 3
 // (profiles/r02/rejected/), a cooperative walk costs 0.47-0.9 VALU per input bit and wave
 // (speculative segments resync slowly on header text: 78 % within 64 bits) against ~0.08 for a lane
 // walk, and a fill of the fill kernel waits for its longest literal, decoded by one lane. So here a
 // literal is decoded by ONE lane with the fill kernel's two-lookup step, and the parallelism comes
 // from decoding tens of thousands of long literals at once:
-//   * one workgroup per CU, no fills and no barriers in the loop: a lane that finishes takes the
-//     next long literal from its wave's LDS queue; a wave whose queue runs dry claims the next 64
-//     entries of the lists (one device-scope atomic), all of the >= long_big class first (a rough
-//     longest-first order: the longest literals start first, the short ones fill in);
+//   * 8 waves per workgroup, no barriers: a lane that finishes takes the next literal from its
+//     wave's LDS queue; a wave whose queue runs dry claims 64 more list entries (the >= long_big
+//     class first: a rough longest-first order);
 //   * each lane streams its literal through an input ring in LDS (dword j of lane t at
 //     ring[j % kRing][t]: conflict-free). Global loads are issued only at wave-uniform refill points,
 //     every kU steps, two 16-byte chunks per lane into registers, and written to the ring at the
@@ -23,12 +26,16 @@
 //     at refill points as 16-byte stores of whole 16-byte groups of the output (a literal's first
 //     and last group bytewise): scattered dword stores straight from the step cost a TA cycle per
 //     lane and dword (0.8 ms of config 3 in the first measurement);
+//   * memory operations are buffer instructions whose operands stay live until the next refill
+//     point (pin): the compiler otherwise reuses a pending store's registers after waiting for the
+//     store, a full memory round trip in the first step of every period;
 //   * a literal that ends is finished (padding check, last bytes, length, status) at the next
 //     refill point, outside the steps.
 // Semantics are the fill kernel's lane walk (huffman.rs:95-161): the walk stops where no code fits,
 // an EOS is EOSInString at once, then >7 residual bits PaddingTooLarge, non-ones InvalidPadding.
 #pragma once
-#include "hpk_decode12.h"
+// (included by hpk_decode12.h after the lane-walk helpers it uses: lut12, residual_status, lo_decode)
+#include "hpk_decode_kernel.h"
 
 namespace hpkdec {
 
@@ -61,76 +68,36 @@ __device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t gb
 // Keep a value's register live (and unchanged) up to here.
 __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 
-// kBlock threads (one workgroup per CU), kU steps between refill points, kRing input dwords and
-// 64 output bytes per lane. kDiag (diagnostic builds): per-wave counters into a.dbg[wave * 16 + i]
-// (scripts/diag_decode.py).
-template <int kBlock, int kU, int kRing, int kDiag = 0>
-__global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t fill_grid) {
-    constexpr int kWaves = kBlock / 64;
+// Long-literal phase of fill workgroup g = blockIdx.x (all kBlockAll threads call it, after the
+// fills; c1 / c2 = its class counts). kBlock threads decode (one wave queue of kQ entries each in
+// s_q), kU steps between refill points, kRing input dwords and 64 output bytes per lane in s_ring /
+// s_out. kDiag (diagnostic builds): per-wave counters into a.dbg[wave * 16 + i] (scripts/diag_decode.py).
+template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll>
+__device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
+                                           uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
+                                           const uint32_t* s_lut, const uint16_t* s_lo) {
     constexpr uint32_t kChunk = 64;            // list entries per claim (one per lane)
     constexpr uint32_t kQ = 2 * kChunk;        // per-wave queue: < 64 left + one claim
     constexpr uint32_t kOB = 64;               // output ring bytes per lane
     constexpr uint32_t kOS = kOB + 4;          // its stride (17 dwords: conflict-free), dummy at kOB
     static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
-    static_assert(kBlock >= 256, "one thread per fill workgroup (<= 256 of them)");
-    __shared__ __attribute__((aligned(16))) uint32_t s_lut[HPK_LUT_SIZE];
-    __shared__ __attribute__((aligned(16))) uint16_t s_lo[HPK_LO_SIZE];
-    __shared__ uint32_t s_ring[kRing * kBlock];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[kOS * kBlock];
-    __shared__ uint4 s_q[kWaves][kQ];          // per wave: literals claimed, not started (index, offsets)
-    __shared__ uint32_t s_b1[257], s_b2[257];  // exclusive prefix of the two classes' counts
-    __shared__ uint32_t s_w1[kWaves], s_w2[kWaves];
+    static_assert(kBlock % 64 == 0 && kBlock <= kBlockAll, "decoding waves");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    {  // class counts per fill workgroup (one thread each), scanned
-        const uint32_t g = tid;
-        const uint32_t c1 = g < fill_grid ? a.long_wg[g] : 0u, c2 = g < fill_grid ? a.long_wg[256 + g] : 0u;
-        uint32_t x1 = c1, x2 = c2;  // inclusive scans within the wave
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y1 = __shfl_up(x1, d), y2 = __shfl_up(x2, d);
-            if (lane >= (uint32_t)d) {
-                x1 += y1;
-                x2 += y2;
-            }
-        }
-        if (lane == 63) {
-            s_w1[wv] = x1;
-            s_w2[wv] = x2;
-        }
-        __syncthreads();
-        for (uint32_t w = 0; w < wv; ++w) {
-            x1 += s_w1[w];
-            x2 += s_w2[w];
-        }
-        if (g < fill_grid) {  // s_b[g] = exclusive prefix; s_b[fill_grid] = the total
-            s_b1[g] = x1 - c1;
-            s_b2[g] = x2 - c2;
-        }
-        if (g == fill_grid - 1u) {
-            s_b1[fill_grid] = x1;
-            s_b2[fill_grid] = x2;
-        }
-    }
-    __syncthreads();
-    const uint32_t total1 = s_b1[fill_grid], total2 = s_b2[fill_grid];
-    if (total1 + total2 == 0) return;  // nothing left to this kernel (config 2 / 5)
-    for (uint32_t t = tid; t < HPK_LUT_SIZE / 4; t += kBlock)
-        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut2)[t];
-    for (uint32_t t = tid; t < (uint32_t)HPK_LO_SIZE * 2 / 16; t += kBlock)
-        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
-    __syncthreads();
+    const uint32_t total = c1 + c2;
+    if (total == 0) return;  // (block-uniform: nothing left to this phase)
+    if (tid >= (uint32_t)kBlock) return;  // (no barrier follows)
+    uint4 (*sq)[kQ] = reinterpret_cast<uint4 (*)[kQ]>(s_q);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     // (whole 16-byte chunks: a load that reaches past num_records reads 0 in all its dwords)
     const __amdgpu_buffer_rsrc_t r_in = buf_rsrc(a.in_base, (in_end + 15u) & ~15u);
     const __amdgpu_buffer_rsrc_t r_out = buf_rsrc(a.out_base, a.out_cap + a.out_mis);
     const __amdgpu_buffer_rsrc_t r_len = buf_rsrc(a.out_len, min(a.n, 0x3FFFFFFFu) * 4u);
     const __amdgpu_buffer_rsrc_t r_st = buf_rsrc(a.status, a.n);
-    const uint32_t nch1 = (total1 + kChunk - 1) / kChunk, nch = nch1 + (total2 + kChunk - 1) / kChunk;
     uint32_t* ring = s_ring + tid;        // input dword j: ring[(j % kRing) * kBlock]
     uint8_t* ob8 = s_out + tid * kOS;     // output byte p: ob8[p % kOB]
     uint8_t* const dmy = ob8 + kOB;
     bool more = true;               // wave-uniform: claims may remain
-    uint32_t qh = 0, qt = 0;        // wave-uniform: the wave's queue s_q[wv][qh, qt) (mod kQ)
+    uint32_t qh = 0, qt = 0;        // wave-uniform: the wave's queue sq[wv][qh, qt) (mod kQ)
     // Lane state. Input positions are relative to the literal's first 16-byte chunk q0: X = bit
     // position + 31 (the fill kernel's convention), the pair (d0, d1) = dwords (X >> 5) - 1 and
     // X >> 5, d2 the next; the ring holds dwords [.., h) (h a multiple of 8), the registers P the next
@@ -243,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
             const uint64_t wm = __ballot(want);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
             if (want && qh + rank < qt) {
-                const uint4 e = s_q[wv][(qh + rank) % kQ];
+                const uint4 e = sq[wv][(qh + rank) % kQ];
                 idx = e.x;
                 act = true;
                 live = false;
@@ -262,39 +229,27 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
             const bool enough = need <= qt - qh;
             qh += min(need, qt - qh);
             if (enough || !more || claims == 2) break;  // (at most two claims per refill point)
-            uint32_t c = 0;
-            if (lane == 0) c = atomicAdd(&a.long_ctr[0], 1u);
-            c = (uint32_t)__builtin_amdgcn_readlane((int)c, 0);
-            if (c >= nch) {
+            // claim the next 64 entries of this workgroup's list (an LDS counter)
+            uint32_t rr = 0;
+            if (lane == 0) rr = atomicAdd(s_claim, kChunk);
+            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rr, 0);
+            if (r >= total) {
                 more = false;
                 break;
             }
-            const bool big = c < nch1;  // wave-uniform
-            const uint32_t v = (big ? c : c - nch1) * kChunk + lane;
-            const uint32_t* sb = big ? s_b1 : s_b2;
-            const bool ok = v < (big ? total1 : total2);
-            // straight-line (no branch around the loads): a load under a branch leaves the compiler
+            // entries r + lane: [0, c1) from the front of the range, then from the back
+            const uint32_t e = r + lane;
+            const bool ok = e < total;
+            const uint32_t lpos = ok ? (e < c1 ? ba + e : bb - 1u - (e - c1)) : ba;
+            const uint32_t i0 = a.long_list[lpos];  // (a load either way: see the note below)
+            const uint32_t i = ok ? i0 : 0u;
+            // straight-line loads (no branch around them): a load under a branch leaves the compiler
             // unsure whether its register is still pending, and it then waits for all memory
             // operations (the refill loads included) before the steps reuse the register
-            const uint32_t vv = ok ? v : 0u;
-            uint32_t r = 0, hi = fill_grid - 1u;  // the last fill workgroup with sb[r] <= vv
-            while (r < hi) {
-                const uint32_t mid = (r + hi + 1u) >> 1;
-                if (sb[mid] <= vv)
-                    r = mid;
-                else
-                    hi = mid - 1u;
-            }
-            const uint32_t e = vv - sb[r];
-            const uint32_t ba = (uint32_t)((uint64_t)a.n * r / fill_grid);
-            const uint32_t bb = (uint32_t)((uint64_t)a.n * (r + 1u) / fill_grid);
-            const uint32_t lpos = ok ? (big ? ba + e : bb - 1u - e) : 0u;
-            const uint32_t i0 = a.long_list[lpos];  // (entry 0 when !ok: a load either way)
-            const uint32_t i = ok ? i0 : 0u;
             const uint4 li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.out_off[i]);
             const uint64_t lm = __ballot(ok);
             const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-            if (ok) s_q[wv][(qt + lr) % kQ] = li;
+            if (ok) sq[wv][(qt + lr) % kQ] = li;
             qt += (uint32_t)__popcll(lm);
         }
         if (kDiag) {
@@ -396,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void hpk_decode_long(DecodeArgs a, uint32_t
     }
     if (kDiag) {
         dg[0] = __builtin_amdgcn_s_memtime() - dt0;
-        const uint32_t gw = blockIdx.x * (uint32_t)kWaves + wv;
+        const uint32_t gw = blockIdx.x * (uint32_t)(kBlock / 64) + wv;
         if (lane < 10) {
             unsigned long long v = 0;
 #pragma unroll
