@@ -1,21 +1,21 @@
 // hpk_long.h — long-literal decode phase (v19): one lane per literal, streaming from HBM.
 //
 // The fill kernel (hpk_decode12 with kLongK) leaves the literals of >= long_min encoded bytes whose
-// region holds the decoded bound (and whole ranges dominated by them) to this phase, which runs in
-// the same launch once a workgroup's fills are done (a second launch cost ~4.8 us on batches with
-// nothing to leave). Fill workgroup g lists its literals in long_list[its literal range): those of
-// >= long_big bytes from the front (c1 of them), the others from the back (c2), publishes the
-// counts with a release flag tagged with the call's epoch, and then decodes them, first its own,
-// then any other workgroup's that has published (claims of 64 entries on a per-workgroup device
-// counter; a workgroup whose list is not published yet decodes its own). Measured on config 3
-// (profiles/r02/rejected/), a cooperative walk costs 0.47-0.9 VALU per input bit and wave
-// (speculative segments resync slowly on header text: 78 % within 64 bits) against ~0.08 for a lane
-// walk, and a fill of the fill kernel waits for its longest literal, decoded by one lane. So here a
-// literal is decoded by ONE lane with the fill kernel's two-lookup step, and the parallelism comes
-// from decoding tens of thousands of long literals at once:
-//   * 8 waves per workgroup, no barriers: a lane that finishes takes the next literal from its
-//     wave's LDS queue; a wave whose queue runs dry claims 64 more list entries (the >= long_big
-//     class first: a rough longest-first order);
+// region holds the decoded bound (and whole ranges dominated by them) to this phase, which the same
+// workgroup runs once its fills are done, on its own literal range: it lists them in
+// long_list[its range), those of >= long_big bytes from the front (c1 of them) and the others from
+// the back (c2), so the longest start first. Measured on config 3 (profiles/r02/rejected/), a
+// cooperative walk costs 0.47-0.9 VALU per input bit and wave (speculative segments resync slowly
+// on header text: 78 % within 64 bits) against ~0.08 for a lane walk, and a fill of the fill
+// kernel waits for its longest literal, decoded by one lane. So here a literal is decoded by ONE
+// lane with the fill kernel's two-lookup step, and the parallelism comes from decoding thousands of
+// long literals at once. Measured and not taken: a separate launch over all workgroups' lists
+// (config 3 0.90 ms, but 4.75 us on every batch with nothing to leave), and claims across
+// workgroups inside the fill kernel (a release fence per workgroup to publish its list: config 2
+// 61.8 us, config 3 1.00 ms).
+//   * 8 waves per workgroup (the other 8 exit), no barriers: a lane that finishes takes the next
+//     literal from its wave's LDS queue; a wave whose queue runs dry claims the next 64 entries of
+//     the list (an LDS counter);
 //   * each lane streams its literal through an input ring in LDS (dword j of lane t at
 //     ring[j % kRing][t]: conflict-free). Global loads are issued only at wave-uniform refill points,
 //     every kU steps, two 16-byte chunks per lane into registers, and written to the ring at the
@@ -31,6 +31,8 @@
 //     store, a full memory round trip in the first step of every period;
 //   * a literal that ends is finished (padding check, last bytes, length, status) at the next
 //     refill point, outside the steps.
+// The regions (LDS of the fill kernel, free after its fills): input rings over the output image,
+// output rings over the input window, wave queues over the fill queue.
 // Semantics are the fill kernel's lane walk (huffman.rs:95-161): the walk stops where no code fits,
 // an EOS is EOSInString at once, then >7 residual bits PaddingTooLarge, non-ones InvalidPadding.
 #pragma once
