@@ -105,6 +105,7 @@ struct EncLds {
     uint32_t code1[256];         // serial path: codes
     uint8_t len1[256];           // serial path: lengths
     uint32_t wf[16], wv[16];     // per-wave scan totals
+    uint32_t dmy[kEB];           // per-thread dummy dword (pass 2's unconditional ORs)
     uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen
 };
 
@@ -256,15 +257,25 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         // literals add nothing) and the bytes it owns: masks, so the byte loops below have no
         // control flow and their table reads issue back to back
         uint32_t bm = 0, vm = 0, em = 0;  // em bit j: byte xt + j is the last of its literal
+        // every literal the thread touches has room for 30 bits per byte (the longest code): pass 2
+        // needs no capacity check
+        auto lit_safe = [&](uint32_t l) {
+            return (S.ooff[l + 1] - S.ooff[l]) * 8u >= 30u * (S.ioff[l + 1] - S.ioff[l]);
+        };
+        bool allsafe = true;
+        bool ends_here = false;  // the thread's last literal ends at its last byte
         if (any) {
             vm = (uint32_t)(((1ull << (x1 - x0)) - 1ull) << (x0 - xt));
+            allsafe = lit_safe(li);
             uint32_t lj = li + 1;
             uint32_t nj = S.ioff[lj];
             while (nj < x1) {
                 bm |= 1u << (nj - xt);
+                allsafe &= lit_safe(lj);
                 nj = S.ioff[++lj];
             }
-            em = (bm >> 1) | (nj == x1 ? 1u << (x1 - 1u - xt) : 0u);
+            ends_here = nj == x1;
+            em = (bm >> 1) | (ends_here ? 1u << (x1 - 1u - xt) : 0u);
         }
         // pass 1: (a literal starts in the thread's bytes, bits since the last start)
         uint32_t f = f0 ? 1u : 0u, v = 0;
@@ -308,7 +319,55 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         // accumulator aligned to the image's dword grid: whole dwords inside the run are plain
         // stores, the run's first and last (shared with neighbouring runs) are ds_or; a code past
         // the literal's capacity is clipped (rare: the caller's capacity below the bound)
-        if (any) {
+        if (__all(allsafe)) {
+            // v3 pass 2 (every literal of the wave's threads has room): per byte, the code is shifted
+            // into a 64-bit accumulator holding the bits of the current image dword on (n of them,
+            // counted from the dword's start: a run that starts mid-dword begins with n zero bits
+            // that the OR leaves alone), and the dword goes out with one ds_or when it is complete —
+            // to the thread's dummy dword when it is not, so the byte loop has no branch but the
+            // literal starts'
+            uint32_t lj = li;
+            uint32_t bp = f0 ? 0u : carry;
+            uint32_t q = S.ooff[li] * 8u + bp;
+            uint32_t dq = q >> 5, n = q & 31u;
+            uint64_t acc = 0;
+            uint32_t* const dmy = &S.dmy[tid];
+#pragma unroll 1
+            for (uint32_t g = 0; g < (uint32_t)kEBytes / 8u; ++g) {
+                const uint32_t lo8 = g == 0 ? wd[0] : g == 1 ? wd[2] : g == 2 ? wd[4] : wd[6];
+                const uint32_t hi8 = g == 0 ? wd[1] : g == 1 ? wd[3] : g == 2 ? wd[5] : wd[7];
+                const uint32_t vm8 = vm >> (8u * g), bm8 = bm >> (8u * g);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t b = ((k < 4 ? lo8 : hi8) >> (8 * (k & 3))) & 0xFFu;
+                    const uint2 cl = S.tab[b];
+                    if ((bm8 >> k) & 1u) {  // a literal starts here: close the previous one's run
+                        if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
+                        S.bits[lj] = bp;
+                        const uint32_t x = xt + 8u * g + (uint32_t)k;
+                        while (S.ioff[lj + 1] <= x) ++lj;  // (empty literals between: bits stay 0)
+                        bp = 0;
+                        q = S.ooff[lj] * 8u;
+                        dq = q >> 5;
+                        n = q & 31u;
+                        acc = 0;
+                    }
+                    const bool own = (vm8 >> k) & 1u;
+                    const uint32_t ln = own ? cl.y : 0u;
+                    acc = (acc << ln) | (own ? cl.x : 0u);
+                    n += ln;
+                    bp += ln;
+                    const bool full = n >= 32u;
+                    atomicOr(full ? &S.img[dq] : dmy, (uint32_t)(acc >> ((n - 32u) & 63u)));
+                    dq += full ? 1u : 0u;
+                    n -= full ? 32u : 0u;
+                }
+            }
+            if (any) {
+                if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
+                if (ends_here) S.bits[lj] = bp;
+            }
+        } else if (any) {
             uint32_t lj = li;
             uint32_t bp = f0 ? 0u : carry;
             uint32_t ob = S.ooff[li] * 8u, cap = S.ooff[li + 1] * 8u - ob;
