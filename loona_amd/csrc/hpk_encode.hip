@@ -277,19 +277,20 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             ends_here = nj == x1;
             em = (bm >> 1) | (ends_here ? 1u << (x1 - 1u - xt) : 0u);
         }
-        // pass 1: (a literal starts in the thread's bytes, bits since the last start)
-        uint32_t f = f0 ? 1u : 0u, v = 0;
+        // pass 1: (a literal starts in the thread's bytes, bits since the last start) = the code
+        // lengths of the owned bytes from the last literal start on (mask cm)
+        const uint32_t f = (f0 || bm) ? 1u : 0u;
+        const uint32_t cm = bm ? vm & ~((1u << (31u - __builtin_clz(bm))) - 1u) : vm;
+        uint32_t v = 0;
 #pragma unroll 1
         for (uint32_t g = 0; g < (uint32_t)kEBytes / 8u; ++g) {  // 8 bytes at a time (register pressure)
             const uint32_t lo8 = g == 0 ? wd[0] : g == 1 ? wd[2] : g == 2 ? wd[4] : wd[6];
             const uint32_t hi8 = g == 0 ? wd[1] : g == 1 ? wd[3] : g == 2 ? wd[5] : wd[7];
-            const uint32_t vm8 = vm >> (8u * g), bm8 = bm >> (8u * g);
+            const uint32_t cm8 = cm >> (8u * g);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const uint32_t ln = S.len1[((k < 4 ? lo8 : hi8) >> (8 * (k & 3))) & 0xFFu];
-                const bool ok = (vm8 >> k) & 1u, st = (bm8 >> k) & 1u;
-                f |= st ? 1u : 0u;
-                v = st ? ln : v + (ok ? ln : 0u);
+                v += ((cm8 >> k) & 1u) ? ln : 0u;
             }
         }
         // segmented exclusive scan over the workgroup: the carry into each thread's first literal

@@ -3,6 +3,7 @@
 per wave of every counter."""
 import collections
 import csv
+import os
 import glob
 import re
 import sys
@@ -12,9 +13,9 @@ data = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "decode" not in k:
+        if os.environ.get("PMC_FILTER", "decode") not in k:
             continue
-        m = re.search(r"(hpk_decode\w*?)I((?:Li\d+E)+)", k)
+        m = re.search(r"(hpk_(?:de|en)code\w*?)I((?:Li\d+E)+)", k)
         if m:
             name = m.group(1) + "<" + ",".join(re.findall(r"Li(\d+)E", m.group(2))) + ">"
         else:
