@@ -96,7 +96,8 @@ def test_random_and_edge_literals(codec):
 
 
 def test_long_literals(codec):
-    """Literals of >= 224 encoded bytes take the wave-cooperative (self-synchronising) path: valid
+    """Long literals (v16: the wave-cooperative path; v19: the long-literal phase, here mostly whole
+    ranges handed over): valid
     ones of every code length, random bytes (padding errors), an EOS in the middle at every bit
     offset class, bad padding after a long valid run, and long runs of 30-bit codes and of ones
     (where speculative starts synchronise late). Bit-exact against the oracle, with short literals
@@ -132,6 +133,109 @@ def test_long_literals(codec):
     lits.append(huffman_encode(bytes(range(256)) * 12))  # every code length
     blob, off = pack(lits)
     compare_batches(gpu_decode(codec, blob, off), oracle_decode_batch(blob, off), "long literals")
+
+
+def _decode_regions(codec, blob, off, caps, shift=0, guard=64):
+    """Decode into caller-chosen region sizes `caps` (back to back), the output buffer surrounded
+    by guard bytes; returns (out, out_off, out_len, status) over the regions and the guard bytes."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    n = len(off) - 1
+    oo = np.zeros(n + 1, np.int64)
+    np.cumsum(np.asarray(caps, np.int64), out=oo[1:])
+    pad = np.zeros(blob.size + shift + 1, np.uint8)
+    pad[shift : shift + blob.size] = blob
+    dblob = to_dev(pad)[shift:]
+    doff = to_dev(np.asarray(off, np.int64).astype(np.int32))
+    big = torch.full((int(oo[-1]) + 2 * guard + shift,), 0xAB, dtype=torch.uint8, device="cuda")
+    out = big[guard + shift : guard + shift + int(oo[-1]) + 1]
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    codec.decode_into(dblob, doff, out, to_dev(oo.astype(np.int32)), ol, st, device=True, sync=True)
+    g = big.cpu().numpy()
+    return (out.cpu().numpy(), oo.astype(np.uint32), ol.cpu().numpy().astype(np.uint32), st.cpu().numpy()), \
+        np.concatenate([g[: guard + shift], g[guard + shift + int(oo[-1]) :]])
+
+
+def test_long_literals_sprinkled_in_short_fills(codec):
+    """v19: literals of >= 64 encoded bytes inside ranges of short ones are left by the fills and
+    decoded after them, one lane each from HBM (hpk_long.h); 1 % of the literals, 64 B - 4 KiB, at
+    random positions, every kind the oracle distinguishes, base pointers at 4 alignments."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(77)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;,/: ", np.uint8)
+    lits = []
+    for i in range(60000):
+        if rng.random() < 0.01:
+            n = int(rng.integers(80, 4000))
+            k = rng.random()
+            if k < 0.6:
+                lits.append(huffman_encode(rng.choice(alpha, n).tobytes()))
+            elif k < 0.8:
+                lits.append(huffman_encode(rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+            elif k < 0.9:
+                body = bytearray(huffman_encode(rng.choice(alpha, n).tobytes()))
+                body[-1] &= 0xF0  # bad padding (or a truncated code)
+                lits.append(bytes(body))
+            else:
+                lits.append(rng.integers(0, 256, n // 2, dtype=np.uint8).tobytes())  # random bits
+        else:
+            lits.append(huffman_encode(rng.choice(alpha, int(rng.integers(0, 60))).tobytes()))
+    blob, off = pack(lits)
+    want = oracle_decode_batch(blob, off)
+    for shift in (0, 5):
+        compare_batches(gpu_decode(codec, blob, off, shift), want, f"sprinkled long literals, shift {shift}")
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_long_literals_exact_bound_regions(codec, shift):
+    """Long literals made only of 5-bit codes fill their region's decoded bound exactly, regions
+    back to back with unrounded capacities and unaligned bases: the long-literal phase's 16-byte
+    group stores and bytewise first/last groups must not touch a neighbour's bytes or the guard."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(5)
+    five = np.frombuffer(b"012aceiost", np.uint8)
+    lits = []
+    for k in range(4000):
+        if k % 3 == 0:
+            lits.append(huffman_encode(rng.choice(five, 8 * int(rng.integers(13, 300))).tobytes()))  # >= 65 B
+        elif k % 3 == 1:
+            lits.append(huffman_encode(rng.choice(five, int(rng.integers(1, 40))).tobytes()))
+        else:
+            lits.append(b"")
+    blob, off = pack(lits)
+    bound = (np.diff(off.astype(np.int64)) * 8) // 5
+    got, guard = _decode_regions(codec, blob, off, bound, shift)
+    compare_batches(got, oracle_decode_batch(blob, off), "long exact-bound regions")
+    assert (got[2].astype(np.int64)[0::3] == bound[0::3]).all()
+    assert (guard == 0xAB).all()
+
+
+def test_dense_range_falls_back_to_fills(codec):
+    """A range dominated by long literals is handed to the long-literal phase whole, unless one of
+    its literals has a region below the decoded bound: then the range is decoded by fills after
+    all, and that literal stops at its capacity (HPK_OUTPUT_OVERFLOW) as on the short path."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(9)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
+    lits = [huffman_encode(rng.choice(alpha, int(rng.integers(300, 3000))).tobytes()) for _ in range(3000)]
+    blob, off = pack(lits)
+    enc = np.diff(off.astype(np.int64))
+    caps = (enc * 8) // 5
+    small = [7, 1500, 2999]
+    caps[small] = 7
+    got, guard = _decode_regions(codec, blob, off, caps)
+    want = oracle_decode_batch(blob, off)
+    keep = np.setdiff1d(np.arange(len(lits)), small)
+    assert (got[3][small] == 4).all() and (got[2][small] == 7).all()
+    assert (got[3][keep] == 0).all() and (got[2][keep] == want[2][keep]).all()
+    for i in small:  # the first 7 bytes are the literal's first 7 decoded bytes
+        assert bytes(got[0][got[1][i] : got[1][i] + 7]) == bytes(want[0][want[1][i] : want[1][i] + 7])
+    for i in keep[::97]:
+        assert bytes(got[0][got[1][i] : got[1][i] + got[2][i]]) == bytes(want[0][want[1][i] : want[1][i] + want[2][i]])
+    assert (guard == 0xAB).all()
 
 
 def test_empty_batch_and_empty_literals(codec):
