@@ -21,18 +21,20 @@
 //     every kU steps, two 16-byte chunks per lane into registers, and written to the ring at the
 //     NEXT refill point: a load has kU steps to land before anything waits on it (a load waited for
 //     where a lane needs it stalls the whole wave for the HBM latency at every 16 bytes);
-//   * decoded bytes go to a 64-byte output ring per lane in LDS (unconditional byte stores, a
-//     lane's dummy byte for the slots a step does not fill, as the fill kernel's kPred) and leave it
-//     at refill points as 16-byte stores of whole 16-byte groups of the output (a literal's first
-//     and last group bytewise): scattered dword stores straight from the step cost a TA cycle per
-//     lane and dword (0.8 ms of config 3 in the first measurement);
+//   * decoded bytes go to a 96-byte output buffer per lane in LDS, a step's bytes as 4 byte
+//     stores at fixed offsets from the lane's position (the buffer is the lane's own: the bytes
+//     past the decoded ones are overwritten later or never stored out; no dummy slot, no address
+//     select), and leave it at refill points as 16-byte stores of
+//     whole 16-byte groups of the output (a literal's first and last group bytewise), the partial
+//     group moved to the buffer's front: scattered dword stores straight from the step cost a TA
+//     cycle per lane and dword (0.8 ms of config 3 in the first measurement);
 //   * memory operations are buffer instructions whose operands stay live until the next refill
 //     point (pin): the compiler otherwise reuses a pending store's registers after waiting for the
 //     store, a full memory round trip in the first step of every period;
 //   * a literal that ends is finished (padding check, last bytes, length, status) at the next
 //     refill point, outside the steps.
-// The regions (LDS of the fill kernel, free after its fills): input rings over the output image,
-// output rings over the input window, wave queues over the fill queue.
+// The regions (LDS of the fill kernel, free after its fills): input rings (64 KiB) and output
+// buffers (48 KiB) over the input window and the output image, wave queues over the fill queue.
 // Semantics are the fill kernel's lane walk (huffman.rs:95-161): the walk stops where no code fits,
 // an EOS is EOSInString at once, then >7 residual bits PaddingTooLarge, non-ones InvalidPadding.
 #pragma once
@@ -72,16 +74,21 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 
 // Long-literal phase of fill workgroup g = blockIdx.x (all kBlockAll threads call it, after the
 // fills; c1 / c2 = its class counts). kBlock threads decode (one wave queue of kQ entries each in
-// s_q), kU steps between refill points, kRing input dwords and 64 output bytes per lane in s_ring /
-// s_out. kDiag (diagnostic builds): per-wave counters into a.dbg[wave * 16 + i] (scripts/diag_decode.py).
+// s_q), kU steps between refill points, kRing input dwords per lane in s_ring and a kOS-byte
+// output buffer per lane in s_out (16-byte aligned). kDiag (diagnostic builds): per-wave counters
+// into a.dbg[wave * 16 + i] (scripts/diag_decode.py).
 template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll>
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
                                            const uint32_t* s_lut, const uint16_t* s_lo) {
     constexpr uint32_t kChunk = 64;            // list entries per claim (one per lane)
     constexpr uint32_t kQ = 2 * kChunk;        // per-wave queue: < 64 left + one claim
-    constexpr uint32_t kOB = 64;               // output ring bytes per lane
-    constexpr uint32_t kOS = kOB + 4;          // its stride (17 dwords: conflict-free), dummy at kOB
+    // Output buffer per lane: bytes [lb, ob) of the output (lb 16-byte aligned) at [0, ob - lb). A
+    // refill point stores every whole 16-byte group and moves the partial one (< 16 bytes) to the
+    // front, so a period starts with <= 15 bytes and adds <= 5 per step: 15 + 5 kU + 3 bytes
+    // (a step's 4-byte store) must fit.
+    constexpr uint32_t kOS = 96;
+    static_assert(15 + 5 * kU + 3 < (int)kOS, "output buffer");
     static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
     static_assert(kBlock % 64 == 0 && kBlock <= kBlockAll, "decoding waves");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -96,18 +103,17 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     const __amdgpu_buffer_rsrc_t r_len = buf_rsrc(a.out_len, min(a.n, 0x3FFFFFFFu) * 4u);
     const __amdgpu_buffer_rsrc_t r_st = buf_rsrc(a.status, a.n);
     uint32_t* ring = s_ring + tid;        // input dword j: ring[(j % kRing) * kBlock]
-    uint8_t* ob8 = s_out + tid * kOS;     // output byte p: ob8[p % kOB]
-    uint8_t* const dmy = ob8 + kOB;
+    uint8_t* const obuf = s_out + tid * kOS;  // output byte p: obuf[p - lb]
     bool more = true;               // wave-uniform: claims may remain
     uint32_t qh = 0, qt = 0;        // wave-uniform: the wave's queue sq[wv][qh, qt) (mod kQ)
     // Lane state. Input positions are relative to the literal's first 16-byte chunk q0: X = bit
     // position + 31 (the fill kernel's convention), the pair (d0, d1) = dwords (X >> 5) - 1 and
     // X >> 5, d2 the next; the ring holds dwords [.., h) (h a multiple of 8), the registers P the next
     // 8. Output positions are byte addresses relative to out_base: o0 the literal's first, ob the
-    // next, fl the first not yet stored to global memory.
+    // next, fl the first not yet stored to global memory, lb the one at the buffer's front.
     bool act = false, live = false, pend = false, done = false;
     uint32_t idx = 0, X = 0, Eb = 0, d0 = 0, d1 = 0, d2 = 0, st = HPK_OK, q0 = 0, span = 0, h = 0;
-    uint32_t o0 = 0, ob = 0, fl = 0;
+    uint32_t o0 = 0, ob = 0, fl = 0, lb = 0;
     u32x4 P0 = {}, P1 = {};
     unsigned long long dg[10] = {};  // kDiag: 0 cycles, 1 points, 2 lane-steps, 3 stalled, 4 idle,
                                      // 5 assign cycles, 6 step cycles, 7 refill cycles, 8 literals
@@ -139,18 +145,17 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             live = true;
         }
         // 3. output to global memory: a literal's first 16-byte group (it shares it with the previous
-        // region) once complete, bytewise; then whole groups as 16-byte stores. Every register a store
-        // reads its data from stays live until after the steps (pin): the compiler reuses a store's
-        // data register only after waiting for the store to complete, which would stall the first
-        // step of every period on a store round trip.
+        // region) once complete, bytewise; then whole groups as 16-byte stores; the partial group
+        // to the buffer's front. Every register a store reads its data from stays live until after
+        // the steps (pin).
         u32x4 gv[4];
         uint32_t hv[4], hb[16], tv[4], tb[16], lv = 0, sv = 0;
         uint32_t ha = 0, ga = 0, ta = 0, ia = 0, ja = 0;  // their addresses (pinned too)
         {
-            const uint32_t gb = fl & ~15u;
+            const uint32_t gb = fl & ~15u;  // (== lb: nothing of the literal is stored yet)
             ha = gb;
             if (act && fl != gb && gb + 16u <= ob) {
-                const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + (gb & (kOB - 1u)));
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(obuf);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) hv[e] = s[e];
 #pragma unroll
@@ -163,7 +168,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             ga = fl;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + ((fl + 16u * k) & (kOB - 1u)));
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(obuf + min((fl - lb) + 16u * k, kOS - 16u));
                 gv[k] = u32x4{s[0], s[1], s[2], s[3]};
             }
             uint32_t ng = 0;
@@ -175,14 +180,19 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 }
             }
             fl += 16u * ng;
+            if (act && fl != lb && (fl & 15u) == 0) {  // the partial group (< 16 bytes) to the front
+                const uint4 v = *reinterpret_cast<const uint4*>(obuf + (fl - lb));
+                *reinterpret_cast<uint4*>(obuf) = v;
+                lb = fl;
+            }
         }
         // 4. a literal that ended in the last steps: padding check, last bytes, length, status
         if (done) {
             if (st == HPK_OK) st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
-            if (ob > fl) {  // [fl, ob) lies in one group
+            if (ob > fl) {  // [fl, ob) lies in one group, at the buffer's front
                 const uint32_t gb = fl & ~15u;
                 ta = gb;
-                const uint32_t* s = reinterpret_cast<const uint32_t*>(ob8 + (gb & (kOB - 1u)));
+                const uint32_t* s = reinterpret_cast<const uint32_t*>(obuf);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) tv[e] = s[e];
 #pragma unroll
@@ -226,6 +236,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 o0 = e.w + a.out_mis;
                 ob = o0;
                 fl = o0;
+                lb = o0 & ~15u;
             }
             const uint32_t need = (uint32_t)__popcll(wm);
             const bool enough = need <= qt - qh;
@@ -266,9 +277,18 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             P1 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u + 16u, 0, 0);
             pend = true;
         }
-        // ---- kU steps while the input ring holds what a step can reach and the output ring has room ----
+        // ---- kU steps while the input ring holds what a step can reach: a step advances < 2 dwords
+        // (<= 24 bits of lookups + a <= 30-bit long code) and reads up to dword (X >> 5) + 3 ----
+#ifndef HPK_LONG_BUDGET
+#define HPK_LONG_BUDGET 1  // 0: the ring check in every step (config 3 1026.9 vs 936.7 us)
+#endif
+        const uint32_t x5 = X >> 5;
+        const uint32_t budget = !(act && live) ? 0u
+                                : h * 4u >= span ? (uint32_t)kU
+                                : x5 + 4u <= h ? min((uint32_t)kU, ((h - x5 - 4u) >> 1) + 1u) : 0u;
         for (int s = 0; s < kU; ++s) {
-            const bool go = act && live && !done && ((X >> 5) + 4u <= h || h * 4u >= span) && ob - fl <= kOB - 5u;
+            const bool go = HPK_LONG_BUDGET ? (uint32_t)s < budget && !done
+                                            : act && live && !done && ((X >> 5) + 4u <= h || h * 4u >= span);
             if (kDiag) {
                 dg[2] += (unsigned long long)__popcll(__ballot(go));
                 dg[3] += (unsigned long long)__popcll(__ballot(act && live && !done && !go));
@@ -290,12 +310,24 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             const uint32_t u2 = lut12(e2, rem2, b1, b2);
             b1 &= cont;
             b2 &= cont;
-            *(a1 ? ob8 + (ob & (kOB - 1u)) : dmy) = (uint8_t)e1;
-            *(a2 ? ob8 + ((ob + 1u) & (kOB - 1u)) : dmy) = (uint8_t)(e1 >> 16);
-            ob += (uint32_t)a1 + (uint32_t)a2;
-            *(b1 ? ob8 + (ob & (kOB - 1u)) : dmy) = (uint8_t)e2;
-            *(b2 ? ob8 + ((ob + 1u) & (kOB - 1u)) : dmy) = (uint8_t)(e2 >> 16);
-            ob += (uint32_t)b1 + (uint32_t)b2;
+            {  // the step's (up to 4) bytes as one unaligned dword store into the lane's own buffer
+               // (bytes past the ones decoded are overwritten later or never stored out)
+                const uint32_t g1 = (uint32_t)a1 + (uint32_t)a2, g2 = (uint32_t)b1 + (uint32_t)b2;
+#ifndef HPK_LONG_U32
+#define HPK_LONG_U32 0  // 1: one unaligned dword store per step (config 3 936.7 vs 889.7 us: gfx950 splits it)
+#endif
+                if (HPK_LONG_U32) {
+                    const uint32_t pk = lut12_bytes(e1, g1) | (lut12_bytes(e2, g2) << (8u * g1));
+                    __builtin_memcpy(obuf + (ob - lb), &pk, 4);
+                } else {  // (byte stores: bytes past the decoded ones land in the buffer, harmless)
+                    uint8_t* const p = obuf + (ob - lb);
+                    p[0] = (uint8_t)e1;
+                    p[1] = (uint8_t)(e1 >> 16);
+                    p[g1] = (uint8_t)e2;
+                    p[g1 + 1] = (uint8_t)(e2 >> 16);
+                }
+                ob += g1 + g2;
+            }
             park |= cont & (e2 < HPK_LUT2_ONE) & (rem2 > (uint32_t)HPK_LUT_BITS);
             const uint32_t xn = X + u1 + (cont ? u2 : 0u);
             const bool cross = (xn ^ X) > 31u;
@@ -316,7 +348,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                     st = HPK_EOS_IN_STRING;
                     prog = false;
                 } else {
-                    ob8[ob & (kOB - 1u)] = (uint8_t)sy;
+                    obuf[ob - lb] = (uint8_t)sy;
                     ob += 1u;
                     X += len;
                     const uint32_t j = X >> 5;
