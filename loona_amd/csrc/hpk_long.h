@@ -28,9 +28,12 @@
 //     whole 16-byte groups of the output (a literal's first and last group bytewise), the partial
 //     group moved to the buffer's front: scattered dword stores straight from the step cost a TA
 //     cycle per lane and dword (0.8 ms of config 3 in the first measurement);
-//   * memory operations are buffer instructions whose operands stay live until the next refill
-//     point (pin): the compiler otherwise reuses a pending store's registers after waiting for the
-//     store, a full memory round trip in the first step of every period;
+//   * memory operations are buffer instructions (one VGPR offset) whose operands stay live until
+//     the next refill point (pin), and the claim's loads are straight-line: the first version had
+//     vmcnt waits for everything (the refill loads included) in the first step of every period,
+//     where the compiler re-used registers it could not prove free of a pending memory operation;
+//   * a lane's step budget for the period is set at the refill point from its ring's lookahead
+//     (a step advances < 2 dwords), not checked in every step;
 //   * a literal that ends is finished (padding check, last bytes, length, status) at the next
 //     refill point, outside the steps.
 // The regions (LDS of the fill kernel, free after its fills): input rings (64 KiB) and output
