@@ -1469,7 +1469,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         lds_barrier();
         if (tid == 0) s_ctr[5] = 0;  // its claim counter
         __syncthreads();  // (every thread's list entries and stores are out)
-        static_assert(kW + kO >= 512 * (32 * 4 + 96) && G::kInOff % 16 == 0 && kW % 16 == 0, "long-phase LDS");
+        static_assert(kW + kO >= 512 * (32 * 4 + HPK_LONG_OS) && G::kInOff % 16 == 0 && kW % 16 == 0, "long-phase LDS");
         long_phase<512, 8, 32, kMode == 5 ? 1 : 0, G::kBlock>(a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5],
                                                               reinterpret_cast<uint32_t*>(s_in), s_in + 512 * 32 * 4,
                                                               reinterpret_cast<uint4*>(s_q), s_lut, s_lo);

@@ -75,6 +75,10 @@ __device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t gb
 // Keep a value's register live (and unchanged) up to here.
 __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 
+#ifndef HPK_LONG_OS
+#define HPK_LONG_OS 80  // output buffer bytes per lane (a multiple of 16; 80: 20-dword stride, 4-way bank aliasing instead of 96's 8-way, config 3 870 vs 883 us)
+#endif
+
 // Long-literal phase of fill workgroup g = blockIdx.x (all kBlockAll threads call it, after the
 // fills; c1 / c2 = its class counts). kBlock threads decode (one wave queue of kQ entries each in
 // s_q), kU steps between refill points, kRing input dwords per lane in s_ring and a kOS-byte
@@ -90,7 +94,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     // refill point stores every whole 16-byte group and moves the partial one (< 16 bytes) to the
     // front, so a period starts with <= 15 bytes and adds <= 5 per step: 15 + 5 kU + 3 bytes
     // (a step's 4-byte store) must fit.
-    constexpr uint32_t kOS = 96;
+    constexpr uint32_t kOS = HPK_LONG_OS;
     static_assert(15 + 5 * kU + 3 < (int)kOS, "output buffer");
     static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
     static_assert(kBlock % 64 == 0 && kBlock <= kBlockAll, "decoding waves");
