@@ -106,6 +106,7 @@ struct EncLds {
     uint8_t len1[256];           // serial path: lengths
     uint32_t wf[16], wv[16];     // per-wave scan totals
     uint32_t dmy[kEB];           // per-thread dummy dword (pass 2's unconditional ORs)
+    uint32_t live[(kEO / 16 + 31) / 32];  // image chunks holding output bytes (the rest is slack)
     uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen
 };
 
@@ -138,6 +139,10 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         S.tab[tid] = make_uint2(c, l);
         S.code1[tid] = c;
         S.len1[tid] = (uint8_t)l;
+    }
+    {  // the image starts clear; every tile clears what it wrote (its live chunks) after storing them
+        uint4* i16 = reinterpret_cast<uint4*>(S.img);
+        for (uint32_t c = tid; c < (uint32_t)kEO / 16; c += kEB) i16[c] = make_uint4(0, 0, 0, 0);
     }
     const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
@@ -176,10 +181,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             S.ctr[0] = 0;
             S.ctr[1] = 0;
         }
-        {  // clear the image
-            uint4* i16 = reinterpret_cast<uint4*>(S.img);
-            for (uint32_t c = tid; c < (uint32_t)kEO / 16; c += kEB) i16[c] = make_uint4(0, 0, 0, 0);
-        }
+        for (uint32_t w = tid; w < (uint32_t)((kEO / 16 + 31) / 32); w += kEB) S.live[w] = 0;
         lds_barrier_e();
         // which literals fit (a prefix: offsets are non-decreasing)
         uint32_t kw = 0;
@@ -443,8 +445,16 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
                     const uint32_t pad = 8u - (bits & 7u);
                     img_or(S.img, S.ooff[t] * 8u + bits, (1u << pad) - 1u, pad);
                 }
-                a.out_len[cur + t] = over ? cap : nbytes;
+                const uint32_t len = over ? cap : nbytes;
+                a.out_len[cur + t] = len;
                 a.status[cur + t] = (uint8_t)(over ? HPK_OUTPUT_OVERFLOW : HPK_OK);
+                if (len) {  // the image chunks holding the output: the only ones stored
+                    const uint32_t ca = S.ooff[t] >> 4, cb = (S.ooff[t] + len - 1u) >> 4;
+                    for (uint32_t w = ca >> 5; w <= cb >> 5; ++w) {
+                        const uint32_t lo = w == (ca >> 5) ? (ca & 31u) : 0u, hi = w == (cb >> 5) ? (cb & 31u) : 31u;
+                        atomicOr(&S.live[w], (0xFFFFFFFFu >> (31u - hi)) & (0xFFFFFFFFu << lo));
+                    }
+                }
             }
         }
         lds_barrier_e();
@@ -453,11 +463,15 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             const uint32_t c1 = (G1 + 15u) >> 4;
             const uint4* i16 = reinterpret_cast<const uint4*>(S.img);
             uint4* g16 = reinterpret_cast<uint4*>(a.out_base + ob16);
+            uint4* m16 = reinterpret_cast<uint4*>(S.img);
             for (uint32_t c = tid; c < c1; c += kEB) {
-                if ((c << 4) >= G0 && (c << 4) + 16u <= G1) {
+                // (live chunks only: with encode_offsets' regions, 30 bits per input byte, most of the
+                // span is slack no byte of output reaches)
+                if ((c << 4) >= G0 && (c << 4) + 16u <= G1 && ((S.live[c >> 5] >> (c & 31u)) & 1u)) {
                     const uint4 w = i16[c];
                     g16[c] = make_uint4(__builtin_bswap32(w.x), __builtin_bswap32(w.y), __builtin_bswap32(w.z),
                                         __builtin_bswap32(w.w));
+                    m16[c] = make_uint4(0, 0, 0, 0);
                 }
             }
             if (tid < 32) {  // the partial chunks at the two ends, one byte per lane
@@ -468,6 +482,8 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
                     const uint32_t w = S.img[x >> 2];
                     a.out_base[ob16 + x] = (uint8_t)(w >> (24u - 8u * (x & 3u)));
                 }
+                // then clear them (wave 0's reads above come first: one wave, program order)
+                if ((tid & 15u) == 0 && partial) m16[g >> 4] = make_uint4(0, 0, 0, 0);
             }
         }
         cur = cur_n;
