@@ -16,6 +16,7 @@
 #include <stdlib.h>
 
 #include "hpk_device.h"
+#include "hpk_split.h"
 
 namespace {
 
@@ -95,11 +96,16 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
 // workgroup's global-memory waits overlap the other's LDS work; 1024 / 112 KiB / 2048 (one per CU)
 // stays for comparison (HPK_ENCODE_CFG=1; 2 and 3: 16 bytes per thread).
 
+// Pass 2's phantom runs (bytes a thread holds but does not own: before the tile's first literal,
+// after its last) go to kEPh dwords past the image: a run covers at most 32 bytes of 30-bit codes
+// (30 dwords), started at dword (tid & 31) so the lanes of a wave do not all hit one address.
+constexpr int kEPh = 64;
+
 template <int kEB, int kEO, int kEQ>
 struct EncLds {
-    uint32_t img[kEO / 4];       // the tile's output span, big-endian dwords
-    uint32_t ioff[kEQ + 1];      // input offsets of the tile's literals, relative to the tile base
-    uint32_t ooff[kEQ + 1];      // output offsets, relative to the image base
+    uint32_t img[kEO / 4 + kEPh];  // the tile's output span, big-endian dwords; then the phantom dwords
+    uint32_t ioff[kEQ + 3];      // input offsets of the tile's literals, relative to the tile base (+ sentinel)
+    uint32_t ooff[kEQ + 2];      // output offsets, relative to the image base
     uint32_t bits[kEQ];          // encoded bits per literal (set by the thread holding its last byte)
     uint2 tab[256];              // (code, length)
     uint32_t code1[256];         // serial path: codes
@@ -108,6 +114,7 @@ struct EncLds {
     uint32_t dmy[kEB];           // per-thread dummy dword (pass 2's unconditional ORs)
     uint32_t live[(kEO / 16 + 31) / 32];  // image chunks holding output bytes (the rest is slack)
     uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen
+    uint32_t split[2 * hpksplit::kMaxRounds];  // split_by_bytes's counters
 };
 
 
@@ -144,8 +151,9 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         uint4* i16 = reinterpret_cast<uint4*>(S.img);
         for (uint32_t c = tid; c < (uint32_t)kEO / 16; c += kEB) i16[c] = make_uint4(0, 0, 0, 0);
     }
-    const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
-    const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+    // the workgroup's literals: equal input bytes (+ 16 per literal) per workgroup
+    uint32_t BA, BB;
+    hpksplit::split_by_bytes<kEB, 16>(a.in_off, a.n, S.split, BA, BB);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;  // (clamped: reads stay in the blob)
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
     const uint4* g_in = reinterpret_cast<const uint4*>(a.in_base);
@@ -220,6 +228,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             break;
         }
         const uint32_t k = S.ctr[0];
+        if (tid == 0) S.ioff[k + 1] = 0xFFFFFFFFu;  // pass 2's literal search stops at the phantom literal k
         if (k == 0) {  // literal `cur` alone exceeds a tile: one lane, global memory
             if (tid == 0) encode_serial(a, S.code1, S.len1, cur);
             cur += 1;
@@ -279,6 +288,11 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             ends_here = nj == x1;
             em = (bm >> 1) | (ends_here ? 1u << (x1 - 1u - xt) : 0u);
         }
+        // pass 2's run starts: the literal starts, the tile's first byte when the thread holds bytes
+        // before it (the run before is a phantom) and the tile's end when the thread holds bytes after
+        // it (the run after is a phantom; x1 < xt + 32 only there)
+        const uint32_t bm2 = bm | (any && x0 > xt ? 1u << (x0 - xt) : 0u) |
+                             (any && x1 < xt + (uint32_t)kEBytes ? 1u << (x1 - xt) : 0u);
         // pass 1: (a literal starts in the thread's bytes, bits since the last start) = the code
         // lengths of the owned bytes from the last literal start on (mask cm)
         const uint32_t f = (f0 || bm) ? 1u : 0u;
@@ -292,7 +306,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const uint32_t ln = S.len1[((k < 4 ? lo8 : hi8) >> (8 * (k & 3))) & 0xFFu];
-                v += ((cm8 >> k) & 1u) ? ln : 0u;
+                v += ln & (uint32_t)__builtin_amdgcn_sbfe((int)cm8, k, 1);  // ln or 0, no select
             }
         }
         // segmented exclusive scan over the workgroup: the carry into each thread's first literal
@@ -329,9 +343,18 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             // that the OR leaves alone), and the dword goes out with one ds_or when it is complete —
             // to the thread's dummy dword when it is not, so the byte loop has no branch but the
             // literal starts'
-            uint32_t lj = li;
-            uint32_t bp = f0 ? 0u : carry;
-            uint32_t q = S.ooff[li] * 8u + bp;
+            // Every byte of the thread is coded (no ownership mask): bytes outside the tile's
+            // literals belong to phantom runs whose dwords land past the image, and the literal's
+            // bit count is the run's end position minus its start (no per-byte count)
+            // the run-start branch advances to the next literal with offsets read at the previous
+            // start (nq: its first bit, nx: the literal after it's first byte; an empty literal
+            // between takes the search)
+            uint32_t lj = any && x0 > xt ? li - 1u : li;
+            uint32_t nq = S.ooff[lj + 1u] * 8u, nx = S.ioff[lj + 2u];
+            bool ph = !any || x0 > xt;  // in a phantom run
+            const uint32_t qph = (uint32_t)(kEO / 4 + (tid & 31u)) * 32u;
+            uint32_t qs = ph ? qph : S.ooff[li] * 8u;  // the run's literal's first bit
+            const uint32_t q = ph ? qph : qs + (f0 ? 0u : carry);
             uint32_t dq = q >> 5, n = q & 31u;
             uint64_t acc = 0;
             uint32_t* const dmy = &S.dmy[tid];
@@ -339,36 +362,45 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             for (uint32_t g = 0; g < (uint32_t)kEBytes / 8u; ++g) {
                 const uint32_t lo8 = g == 0 ? wd[0] : g == 1 ? wd[2] : g == 2 ? wd[4] : wd[6];
                 const uint32_t hi8 = g == 0 ? wd[1] : g == 1 ? wd[3] : g == 2 ? wd[5] : wd[7];
-                const uint32_t vm8 = vm >> (8u * g), bm8 = bm >> (8u * g);
+                const uint32_t bm8 = bm2 >> (8u * g);
+                // the group's table reads issue together, ahead of the run-start branches (which
+                // would otherwise hold each read back to its own byte)
+                uint2 tb[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t b = ((k < 4 ? lo8 : hi8) >> (8 * (k & 3))) & 0xFFu;
-                    const uint2 cl = S.tab[b];
-                    if ((bm8 >> k) & 1u) {  // a literal starts here: close the previous one's run
+                for (int j = 0; j < 8; ++j) tb[j] = S.tab[((j < 4 ? lo8 : hi8) >> (8 * (j & 3))) & 0xFFu];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint2 cl = tb[j];
+                    if ((bm8 >> j) & 1u) {  // a run starts here: close the previous one
                         if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
-                        S.bits[lj] = bp;
-                        const uint32_t x = xt + 8u * g + (uint32_t)k;
-                        while (S.ioff[lj + 1] <= x) ++lj;  // (empty literals between: bits stay 0)
-                        bp = 0;
-                        q = S.ooff[lj] * 8u;
-                        dq = q >> 5;
-                        n = q & 31u;
+                        if (!ph) S.bits[lj] = dq * 32u + n - qs;
+                        const uint32_t x = xt + 8u * g + (uint32_t)j;
+                        if (nx > x) {
+                            ++lj;
+                            qs = nq;
+                        } else {
+                            while (S.ioff[lj + 1] <= x) ++lj;  // (empty literals between: bits stay 0)
+                            qs = S.ooff[lj] * 8u;
+                        }
+                        ph = lj >= k;  // (k: the tile's literals) the tile's end: the rest is a phantom
+                        qs = ph ? qph : qs;
+                        nq = S.ooff[lj + 1u] * 8u;
+                        nx = S.ioff[lj + 2u];
+                        dq = qs >> 5;
+                        n = qs & 31u;
                         acc = 0;
                     }
-                    const bool own = (vm8 >> k) & 1u;
-                    const uint32_t ln = own ? cl.y : 0u;
-                    acc = (acc << ln) | (own ? cl.x : 0u);
-                    n += ln;
-                    bp += ln;
+                    acc = (acc << cl.y) | cl.x;
+                    n += cl.y;
                     const bool full = n >= 32u;
                     atomicOr(full ? &S.img[dq] : dmy, (uint32_t)(acc >> ((n - 32u) & 63u)));
                     dq += full ? 1u : 0u;
-                    n -= full ? 32u : 0u;
+                    n &= 31u;  // (n < 62)
                 }
             }
-            if (any) {
+            if (any && !ph) {
                 if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
-                if (ends_here) S.bits[lj] = bp;
+                if (ends_here) S.bits[lj] = dq * 32u + n - qs;
             }
         } else if (any) {
             uint32_t lj = li;
