@@ -36,7 +36,17 @@ struct EncodeArgs {
     uint32_t out_mis;
     uint32_t in_cap, out_cap;  // blob sizes (clamped to HPK_MAX_OFFSET): larger offsets are bad
     uint32_t* err;             // sticky error flag (host-mapped): set to 1 on bad offsets
+    unsigned long long* prof;  // diagnostic build: cycles per kernel phase (kProf)
 };
+
+// diagnostic build: per-wave cycles spent in each phase of hpk_encode2, summed over waves
+
+#define EPROF(i)                                                                  \
+    if (kProf) {                                                                  \
+        const uint64_t now_ = clock64();                                          \
+        if (lane == 0) atomicAdd(&S.prof[wv][i], (unsigned long long)(now_ - tprev)); \
+        tprev = now_;                                                             \
+    }
 
 // One literal, one lane, global memory: v1's loop (also the large-literal path of v2).
 __device__ __forceinline__ void encode_serial(const EncodeArgs& a, const uint32_t* code, const uint8_t* len,
@@ -101,7 +111,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
 // (30 dwords), started at dword (tid & 31) so the lanes of a wave do not all hit one address.
 constexpr int kEPh = 64;
 
-template <int kEB, int kEO, int kEQ>
+template <int kEB, int kEO, int kEQ, int kP = 0>
 struct EncLds {
     uint32_t img[kEO / 4 + kEPh];  // the tile's output span, big-endian dwords; then the phantom dwords
     uint32_t ioff[kEQ + 3];      // input offsets of the tile's literals, relative to the tile base (+ sentinel)
@@ -111,10 +121,10 @@ struct EncLds {
     uint32_t code1[256];         // serial path: codes
     uint8_t len1[256];           // serial path: lengths
     uint32_t wf[16], wv[16];     // per-wave scan totals
-    uint32_t dmy[kEB];           // per-thread dummy dword (pass 2's unconditional ORs)
     uint32_t live[(kEO / 16 + 31) / 32];  // image chunks holding output bytes (the rest is slack)
     uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen
     uint32_t split[2 * hpksplit::kMaxRounds];  // split_by_bytes's counters
+    unsigned long long prof[kP ? 16 : 1][10];   // diagnostic build (kProf): per-wave phase cycles
 };
 
 
@@ -131,16 +141,19 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
     }
 }
 
-template <int kEB, int kEO, int kEQ, int kEBytes = 32>  // kEBytes: input bytes per thread per tile (16 or 32)
-__global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
+template <int kEB, int kEO, int kEQ, int kEBytes = 32, int kProf = 0>  // kEBytes: input bytes per thread per tile (16 or 32)
+// (at least 4 waves per SIMD: two 512-thread workgroups per CU fit only under 128 VGPRs)
+__global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
     static_assert(kEBytes == 16 || kEBytes == 32, "bytes per thread");
     constexpr int kCh = kEBytes / 16;  // 16-byte chunks per thread
     constexpr int kETile = kEB * kEBytes;  // input bytes per tile
     constexpr int kEMeta = kEQ / kEB;      // offset rounds per thread
-    static_assert(sizeof(EncLds<kEB, kEO, kEQ>) <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+    static_assert(sizeof(EncLds<kEB, kEO, kEQ, kProf>) <= 163840, "LDS budget (160 KiB per CU on gfx950)");
     static_assert(kEB <= 1024 && kEQ % kEB == 0, "geometry");
-    __shared__ __attribute__((aligned(16))) EncLds<kEB, kEO, kEQ> S;
+    __shared__ __attribute__((aligned(16))) EncLds<kEB, kEO, kEQ, kProf> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    uint64_t tprev = kProf ? clock64() : 0;
+    if (kProf && tid < 160) (&S.prof[0][0])[tid] = 0;
     if (tid < 256) {
         const uint32_t c = a.codes[tid], l = a.codes[257 + tid];
         S.tab[tid] = make_uint2(c, l);
@@ -154,6 +167,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
     // the workgroup's literals: equal input bytes (+ 16 per literal) per workgroup
     uint32_t BA, BB;
     hpksplit::split_by_bytes<kEB, 16>(a.in_off, a.n, S.split, BA, BB);
+    EPROF(8);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;  // (clamped: reads stay in the blob)
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
     const uint4* g_in = reinterpret_cast<const uint4*>(a.in_base);
@@ -191,6 +205,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         }
         for (uint32_t w = tid; w < (uint32_t)((kEO / 16 + 31) / 32); w += kEB) S.live[w] = 0;
         lds_barrier_e();
+        EPROF(0);
         // which literals fit (a prefix: offsets are non-decreasing)
         uint32_t kw = 0;
         bool bad = false;  // a literal of the tile's range with decreasing offsets or offsets past a capacity
@@ -227,6 +242,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             if (tid == 0) *a.err = 1u;
             break;
         }
+        EPROF(1);
         const uint32_t k = S.ctr[0];
         if (tid == 0) S.ioff[k + 1] = 0xFFFFFFFFu;  // pass 2's literal search stops at the phantom literal k
         if (k == 0) {  // literal `cur` alone exceeds a tile: one lane, global memory
@@ -293,6 +309,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         // it (the run after is a phantom; x1 < xt + 32 only there)
         const uint32_t bm2 = bm | (any && x0 > xt ? 1u << (x0 - xt) : 0u) |
                              (any && x1 < xt + (uint32_t)kEBytes ? 1u << (x1 - xt) : 0u);
+        EPROF(2);
         // pass 1: (a literal starts in the thread's bytes, bits since the last start) = the code
         // lengths of the owned bytes from the last literal start on (mask cm)
         const uint32_t f = (f0 || bm) ? 1u : 0u;
@@ -309,6 +326,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
                 v += ln & (uint32_t)__builtin_amdgcn_sbfe((int)cm8, k, 1);  // ln or 0, no select
             }
         }
+        EPROF(3);
         // segmented exclusive scan over the workgroup: the carry into each thread's first literal
         uint32_t fi = f, vi = v;
 #pragma unroll
@@ -324,8 +342,12 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             S.wv[wv] = vi;
         }
         lds_barrier_e();
-        uint32_t cw = 0;  // carry into this wave's lane 0
-        for (uint32_t j = 0; j < wv; ++j) cw = S.wf[j] ? S.wv[j] : cw + S.wv[j];
+        uint32_t cw = 0;  // carry into this wave's lane 0 (the waves' totals read together)
+#pragma unroll
+        for (uint32_t j = 0; j < (uint32_t)kEB / 64u - 1u; ++j) {
+            const uint32_t f = S.wf[j], v = S.wv[j];
+            if (j < wv) cw = f ? v : cw + v;
+        }
         uint32_t ef = __shfl_up(fi, 1), ev = __shfl_up(vi, 1);
         if (lane == 0) {
             ef = 0;
@@ -336,19 +358,18 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
         // accumulator aligned to the image's dword grid: whole dwords inside the run are plain
         // stores, the run's first and last (shared with neighbouring runs) are ds_or; a code past
         // the literal's capacity is clipped (rare: the caller's capacity below the bound)
+        EPROF(4);
         if (__all(allsafe)) {
             // v3 pass 2 (every literal of the wave's threads has room): per byte, the code is shifted
             // into a 64-bit accumulator holding the bits of the current image dword on (n of them,
             // counted from the dword's start: a run that starts mid-dword begins with n zero bits
-            // that the OR leaves alone), and the dword goes out with one ds_or when it is complete —
-            // to the thread's dummy dword when it is not, so the byte loop has no branch but the
-            // literal starts'
-            // Every byte of the thread is coded (no ownership mask): bytes outside the tile's
-            // literals belong to phantom runs whose dwords land past the image, and the literal's
-            // bit count is the run's end position minus its start (no per-byte count)
-            // the run-start branch advances to the next literal with offsets read at the previous
-            // start (nq: its first bit, nx: the literal after it's first byte; an empty literal
-            // between takes the search)
+            // that the OR leaves alone), and the dword's bits so far go out with one ds_or per byte,
+            // so the byte loop has no branch but the run starts'. Every byte of the thread is coded
+            // (no ownership mask): bytes outside the tile's literals belong to phantom runs whose
+            // dwords land past the image, and a literal's bit count is its run's end position minus
+            // its start (no per-byte count). The run-start branch advances to the next literal with
+            // offsets read at the previous start (nq: its first bit, nx: the first byte of the
+            // literal after it; an empty literal between takes the search).
             uint32_t lj = any && x0 > xt ? li - 1u : li;
             uint32_t nq = S.ooff[lj + 1u] * 8u, nx = S.ioff[lj + 2u];
             bool ph = !any || x0 > xt;  // in a phantom run
@@ -357,7 +378,6 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             const uint32_t q = ph ? qph : qs + (f0 ? 0u : carry);
             uint32_t dq = q >> 5, n = q & 31u;
             uint64_t acc = 0;
-            uint32_t* const dmy = &S.dmy[tid];
 #pragma unroll 1
             for (uint32_t g = 0; g < (uint32_t)kEBytes / 8u; ++g) {
                 const uint32_t lo8 = g == 0 ? wd[0] : g == 1 ? wd[2] : g == 2 ? wd[4] : wd[6];
@@ -391,11 +411,13 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
                         acc = 0;
                     }
                     acc = (acc << cl.y) | cl.x;
-                    n += cl.y;
+                    n += cl.y;  // 5 <= n < 62
+                    // the current dword's bits so far — all of them once it is complete — ORed in
+                    // every byte (a prefix ORs nothing the complete dword does not)
+                    atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
                     const bool full = n >= 32u;
-                    atomicOr(full ? &S.img[dq] : dmy, (uint32_t)(acc >> ((n - 32u) & 63u)));
                     dq += full ? 1u : 0u;
-                    n &= 31u;  // (n < 62)
+                    n &= 31u;
                 }
             }
             if (any && !ph) {
@@ -464,6 +486,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             flush_run();
         }
         lds_barrier_e();
+        EPROF(5);
         // per literal: EOS padding, out_len, status
 #pragma unroll
         for (int r = 0; r < kEMeta; ++r) {
@@ -490,6 +513,7 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
             }
         }
         lds_barrier_e();
+        EPROF(6);
         {  // write the image back: bytes [G0, G1) of the image (relative to ob16)
             const uint32_t G0 = S.ooff[0], G1 = S.ooff[k];
             const uint32_t c1 = (G1 + 15u) >> 4;
@@ -518,14 +542,20 @@ __global__ __launch_bounds__(kEB) void hpk_encode2(EncodeArgs a) {
                 if ((tid & 15u) == 0 && partial) m16[g >> 4] = make_uint4(0, 0, 0, 0);
             }
         }
+        EPROF(7);
         cur = cur_n;
         gin = gin_n;
         gout = gout_n;
+    }
+    if (kProf) {
+        __syncthreads();
+        if (tid < (kEB / 64) * 9) atomicAdd(&a.prof[tid % 9], S.prof[tid / 9][tid % 9]);
     }
 }
 
 #ifdef HPK_DIAG
 static int g_encode_v1 = -1, g_encode_cfg = 0;
+static unsigned long long* g_eprof = nullptr;  // HPK_ENCODE_PROF=1: hpk_encode2's phase cycles
 #endif
 
 }  // namespace
@@ -540,6 +570,7 @@ int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
+    a.prof = nullptr;
     int cfg = 0;
 #ifdef HPK_DIAG
     // diagnostic build only: v1 (one lane per literal, no offset checks) and geometry variants
@@ -577,6 +608,12 @@ int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
         case 3:  // two 512-thread workgroups per CU, 16 bytes per thread
             hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 16>), grid, dim3(512), 0, c->stream, a);
             break;
+        case 9:  // the product geometry with per-phase cycle counters (hpk_debug_encode_prof)
+            if (!g_eprof) HIP_TRY(hipMalloc(&g_eprof, 16 * sizeof(unsigned long long)));
+            HIP_TRY(hipMemsetAsync(g_eprof, 0, 16 * sizeof(unsigned long long), c->stream));
+            a.prof = g_eprof;
+            hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 32, 1>), grid, dim3(512), 0, c->stream, a);
+            break;
 #endif
         default:  // product: two 512-thread workgroups per CU, 32 bytes per thread
             hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 32>), grid, dim3(512), 0, c->stream, a);
@@ -584,3 +621,11 @@ int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
 }
+
+#ifdef HPK_DIAG
+// diagnostic build: the phase cycles of the last HPK_ENCODE_CFG=9 launch (16 x u64)
+extern "C" int hpk_debug_encode_prof(unsigned long long* host16) {
+    if (!g_eprof) return -1;
+    return hipMemcpy(host16, g_eprof, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
