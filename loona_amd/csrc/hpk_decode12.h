@@ -26,6 +26,14 @@
 //     below), so a 4 KiB header value no longer holds a fill for thousands of steps.
 #pragma once
 #include "hpk_decode_kernel.h"
+#include "hpk_split.h"
+
+#ifndef HPK_DEC_SPLIT
+// workgroup ranges balanced by encoded bytes (hpk_split.h): off — measured on config 3 at 857-861 us
+// against 859-871 (the fills and the long phase already even the workgroups out) and on config 2
+// +4.5 us (the search's two dependent reads before the first fill), profiles/r02/v20/decode_split_ab.jsonl
+#define HPK_DEC_SPLIT 0
+#endif
 
 namespace hpkdec {
 
@@ -868,8 +876,16 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
+#if HPK_DEC_SPLIT
+    // the workgroup's literals: equal encoded bytes (+ 8 per literal) per workgroup (the lane
+    // queue's LDS holds the search's counters; it is set up after)
+    uint32_t BA, BB;
+    hpksplit::split_by_bytes<G::kBlock, 8>(a.in_off, a.n, reinterpret_cast<uint32_t*>(s_q), BA, BB);
+    __syncthreads();
+#else
     const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+#endif
     // offsets are clamped to the input capacity wherever they bound a read, so bad offsets (caught
     // per fill below) never move a window past the blob
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
