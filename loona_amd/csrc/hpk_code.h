@@ -56,12 +56,14 @@ static const uint8_t HPK_CODE_LEN[HPK_NSYM] = {
     30,                                                             /* EOS      */
 };
 
-// LUT2: the LUT's content in the layout of the bit-position step (decode v12), chosen so the step
-// needs one compare per field and v_perm gathers the two symbols:
-//   [7:0] sym0  [12:8] len0  [23:16] sym1  [28:24] len0+len1  [30] one code  [31:30] = 3: two
-// so e >= HPK_LUT2_ONE  <=> at least one code, e >= HPK_LUT2_TWO <=> two codes.
-#define HPK_LUT2_ONE 0x40000000u
-#define HPK_LUT2_TWO 0xC0000000u
+// LUT2: the LUT's content in the layout of the bit-position step (decode v12, fields widened in
+// v20), chosen so the step clamps the bits left to 31 and needs one compare per code, and v_perm
+// gathers the two symbols:
+//   [7:0] sym0  [13:8] len0  [23:16] sym1  [29:24] len0+len1  [30] fewer than two  [31] none
+// a length field of a code the entry does not hold is 63 (never <= the clamped bits left).
+#define HPK_LUT2_NOTTWO 0x40000000u  // e >= : fewer than two codes
+#define HPK_LUT2_NONE 0xC0000000u    // e >= : no code (a 13..30-bit code or EOS starts here)
+#define HPK_LUT2_MISSING 63u         // the length field of a code the entry does not hold
 
 struct hpk_tables {
     uint32_t code[HPK_NSYM];   // right-aligned canonical code
@@ -130,7 +132,11 @@ static inline int hpk_build_tables(hpk_tables* t) {
             int L = t->len[s];
             if (L <= HPK_LUT_BITS && (w >> (32 - L)) == t->code[s]) { s0 = s; l0 = L; break; }
         }
-        if (s0 < 0) { t->lut[v] = 0; t->lut2[v] = 0; continue; }
+        if (s0 < 0) {
+            t->lut[v] = 0;
+            t->lut2[v] = HPK_LUT2_NONE | (HPK_LUT2_MISSING << 8) | (HPK_LUT2_MISSING << 24);
+            continue;
+        }
         uint32_t w1 = w << l0;
         int rem = HPK_LUT_BITS - l0, s1 = -1, l1 = 0;
         for (int s = 0; s < 256 && rem >= 5; ++s) {
@@ -141,10 +147,10 @@ static inline int hpk_build_tables(hpk_tables* t) {
         uint32_t e2 = (uint32_t)s0 | ((uint32_t)l0 << 8);
         if (s1 >= 0) {
             e |= ((uint32_t)s1 << 8) | ((uint32_t)(l0 + l1) << 21) | (2u << 26);
-            e2 |= ((uint32_t)s1 << 16) | ((uint32_t)(l0 + l1) << 24) | HPK_LUT2_TWO;
+            e2 |= ((uint32_t)s1 << 16) | ((uint32_t)(l0 + l1) << 24);
         } else {
             e |= ((uint32_t)l0 << 21) | (1u << 26);
-            e2 |= ((uint32_t)l0 << 24) | HPK_LUT2_ONE;
+            e2 |= (HPK_LUT2_MISSING << 24) | HPK_LUT2_NOTTWO;
         }
         t->lut[v] = e;
         t->lut2[v] = e2;

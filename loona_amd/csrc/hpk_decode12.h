@@ -114,9 +114,11 @@ __device__ __forceinline__ void wc_adv(WinCur& c, uint32_t n, uint32_t d3) {
 // The codes one table entry decodes with rem bits left: ok1 / ok2 = its first / second code fits
 // inside the literal; returns the bits they use.
 __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
-    const uint32_t l1 = (e >> 8) & 31u, t1 = (e >> 24) & 31u;
-    ok1 = (e >= HPK_LUT2_ONE) & (l1 <= rem);
-    ok2 = ok1 & (e >= HPK_LUT2_TWO) & (t1 <= rem);
+    // a length field the entry does not hold is 63, past any clamped rem (and t1 >= l1: ok2 => ok1)
+    const uint32_t rc = min(rem, 31u);
+    const uint32_t l1 = (e >> 8) & 63u, t1 = (e >> 24) & 63u;
+    ok1 = l1 <= rc;
+    ok2 = t1 <= rc;
     return ok2 ? t1 : (ok1 ? l1 : 0u);
 }
 
@@ -191,8 +193,9 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     bool a1, a2;
     const uint32_t u1 = lut12(e1, rem, a1, a2);
     uint32_t use = u1;
-    // a code longer than 12 bits (or EOS) starts here and may still fit
-    bool park = (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);
+    // a code longer than 12 bits (or EOS) starts here and may still fit (with more than 12 bits
+    // left, any code the entry holds fits: no first code <=> the entry has none)
+    bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
     uint32_t pk = 0, g = 0;
     if (!kAcc && kStore == kPred) {
         out8[a1 ? L.o : dmy] = (uint8_t)e1;
@@ -208,12 +211,13 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     }
     if (kLook == 2) {
         // the first entry was consumed whole: look the next bits up too
-        const bool cont = a1 & (a2 | (e1 < HPK_LUT2_TWO));
+        const bool cont = a1 & (a2 | (e1 >= HPK_LUT2_NOTTWO));
         const uint32_t w2 = w << u1;
         const uint32_t rem2 = rem - u1;
         const uint32_t e2 = lut[w2 >> (32 - HPK_LUT_BITS)];
         bool b1, b2;
         const uint32_t u2 = lut12(e2, rem2, b1, b2);
+        park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
         b1 &= cont;
         b2 &= cont;
         if (!kAcc && kStore == kPred) {
@@ -230,7 +234,6 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
             g += g2;
         }
         use += cont ? u2 : 0u;
-        park |= cont & (e2 < HPK_LUT2_ONE) & (rem2 > (uint32_t)HPK_LUT_BITS);
     }
     if (kAcc) acc_push<kStore>(L, out32, pk, g, dmy >> 2);
     const uint32_t xn = L.X + use;
@@ -313,18 +316,18 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
         lut12(e1, rem, a1, a2);
         uint32_t adv = 0;
         if (a1) {
-            const uint32_t l1 = (e1 >> 8) & 31u;
+            const uint32_t l1 = (e1 >> 8) & 63u;
             if (kWrite) put8(out8, o + cnt, e1, oend, kStore);
             cnt += 1;
             if (a2 && pos + l1 < e) {  // the second code also starts inside the segment
                 if (kWrite) put8(out8, o + cnt, e1 >> 16, oend, kStore);
                 cnt += 1;
-                adv = (e1 >> 24) & 31u;
+                adv = (e1 >> 24) & 63u;
             } else {
                 adv = l1;
             }
             run = pos + adv < e;
-        } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
+        } else if (e1 >= HPK_LUT2_NONE && rem > (uint32_t)HPK_LUT_BITS) {
             uint32_t s, len;
             bool eos;
             lo_decode(w, lo, s, len, eos);
@@ -398,16 +401,16 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
         bool a1, a2;
         lut12(e1, rem, a1, a2);
         if (a1) {
-            const uint32_t p2 = pos + ((e1 >> 8) & 31u);
+            const uint32_t p2 = pos + ((e1 >> 8) & 63u);
             r.cnt += 1;
             r.pos = p2;
             if (a2 && p2 < e) {  // the second code also starts inside the segment
                 if (join(p2)) break;
                 r.cnt += 1;
-                r.pos = pos + ((e1 >> 24) & 31u);
+                r.pos = pos + ((e1 >> 24) & 63u);
             }
             run = r.pos < e;
-        } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
+        } else if (e1 >= HPK_LUT2_NONE && rem > (uint32_t)HPK_LUT_BITS) {
             uint32_t sy, len;
             bool eos;
             lo_decode(w, lo, sy, len, eos);
@@ -476,9 +479,9 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
             lut12(e1, rem, a1, a2);
             uint32_t adv = 0;
             if (a1) {
-                const uint32_t l1 = (e1 >> 8) & 31u;
-                adv = (a2 && p + l1 < s0) ? (e1 >> 24) & 31u : l1;
-            } else if (e1 < HPK_LUT2_ONE && rem > (uint32_t)HPK_LUT_BITS) {
+                const uint32_t l1 = (e1 >> 8) & 63u;
+                adv = (a2 && p + l1 < s0) ? (e1 >> 24) & 63u : l1;
+            } else if (e1 >= HPK_LUT2_NONE && rem > (uint32_t)HPK_LUT_BITS) {
                 uint32_t sy, len;
                 bool eos;
                 lo_decode(w, lo, sy, len, eos);
@@ -597,10 +600,10 @@ __device__ __forceinline__ void walk2(const uint32_t* __restrict__ win32, const 
         const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
         const uint32_t kk = __clz(~w);
         const uint32_t el = lo_tab[min(kk, (uint32_t)HPK_LO_RUNS - 1u) * 32u + ((w << ((kk + 1u) & 31u)) >> 27)];
-        const uint32_t l1 = (e1 >> 8) & 31u, t1 = (e1 >> 24) & 31u;
-        const bool ok1 = (e1 >= HPK_LUT2_ONE) & (l1 <= rem);
+        const uint32_t l1 = (e1 >> 8) & 63u, t1 = (e1 >> 24) & 63u;
+        const bool ok1 = (e1 < HPK_LUT2_NONE) & (l1 <= rem);
         const uint32_t i2 = i0 + l1;
-        bool ok2 = ok1 & (e1 >= HPK_LUT2_TWO) & (t1 <= rem) & (s0 + i2 < e);  // the second code starts in the segment
+        bool ok2 = ok1 & (e1 < HPK_LUT2_NOTTWO) & (t1 <= rem) & (s0 + i2 < e);  // the second code starts in the segment
         bool jn2 = false;
         if (kJoin) {
             jn2 = ok2 & (((omask >> (i2 & 63u)) & 1ull) != 0ull);
@@ -608,7 +611,7 @@ __device__ __forceinline__ void walk2(const uint32_t* __restrict__ win32, const 
         }
         const bool eos = (kk >= (uint32_t)HPK_LO_RUNS) | ((el & 0x1FFu) == HPK_EOS);
         const uint32_t llen = eos ? 30u : (el >> 9);
-        const bool lng = !ok1 & (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);  // a 13..30-bit code (or EOS)
+        const bool lng = !ok1 & (e1 >= HPK_LUT2_NONE) & (rem > (uint32_t)HPK_LUT_BITS);  // a 13..30-bit code (or EOS)
         const bool lok = lng & !eos & (llen <= rem);
         const uint32_t v = ok1 ? (ok2 ? ((e1 & 0xFFu) | ((e1 >> 8) & 0xFF00u)) : (e1 & 0xFFu)) : (lok ? (el & 0xFFu) : 0u);
         st128_put(lo, hi, cnt, v);
@@ -1413,8 +1416,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                                 L.act = false;
                             }
                         }
+                        // (only a finish changes what is left: the check stays off the step path;
+                        // an idle lane makes no progress, so the first pass always gets here)
+                        if (!__any(L.act || nv)) break;
                     }
-                    if (!__any(L.act || nv)) break;
                 }
             }
         };

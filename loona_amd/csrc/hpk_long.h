@@ -308,13 +308,14 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             const uint32_t e1 = s_lut[w >> (32 - HPK_LUT_BITS)];
             bool a1, a2;
             const uint32_t u1 = lut12(e1, rem, a1, a2);
-            bool park = (e1 < HPK_LUT2_ONE) & (rem > (uint32_t)HPK_LUT_BITS);
-            const bool cont = a1 & (a2 | (e1 < HPK_LUT2_TWO));
+            bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);  // (see lit12_step)
+            const bool cont = a1 & (a2 | (e1 >= HPK_LUT2_NOTTWO));
             const uint32_t w2 = w << u1;
             const uint32_t rem2 = rem - u1;
             const uint32_t e2 = s_lut[w2 >> (32 - HPK_LUT_BITS)];
             bool b1, b2;
             const uint32_t u2 = lut12(e2, rem2, b1, b2);
+            park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
             b1 &= cont;
             b2 &= cont;
             {  // the step's (up to 4) bytes as one unaligned dword store into the lane's own buffer
@@ -335,7 +336,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 }
                 ob += g1 + g2;
             }
-            park |= cont & (e2 < HPK_LUT2_ONE) & (rem2 > (uint32_t)HPK_LUT_BITS);
             const uint32_t xn = X + u1 + (cont ? u2 : 0u);
             const bool cross = (xn ^ X) > 31u;
             d0 = cross ? d1 : d0;
