@@ -28,6 +28,12 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_RELOAD
+// 1: lane steps read the window's two dwords each step instead of shifting a 3-dword register window
+// (5 fewer VALU per step, but the read sits on the step's dependency chain: config 2 46.2 vs 45.6 us,
+// config 3 825-829 vs 832-842 us, profiles/r02/v20/decode_reload_ab.jsonl)
+#define HPK_RELOAD 0
+#endif
 #ifndef HPK_DEC_SPLIT
 // workgroup ranges balanced by encoded bytes (hpk_split.h): off — measured on config 3 at 857-861 us
 // against 859-871 (the fills and the long phase already even the workgroups out) and on config 2
@@ -186,8 +192,14 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
                                            const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8,
                                            uint32_t dmy = 0) {
     uint32_t* out32 = reinterpret_cast<uint32_t*>(out8);
+#if HPK_RELOAD
+    // the window's two dwords read at each step (no registers shifted on a dword crossing)
+    const uint32_t* const wq = win32 + (L.X >> 5);
+    const uint32_t w = __builtin_amdgcn_alignbit(wq[-1], wq[0], ~L.X);
+#else
     const uint32_t d3 = win32[(L.X >> 5) + 2];  // the dword after d2, in case this step crosses one
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+#endif
     const uint32_t rem = L.Eb - L.X;
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
     bool a1, a2;
@@ -237,14 +249,21 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     }
     if (kAcc) acc_push<kStore>(L, out32, pk, g, dmy >> 2);
     const uint32_t xn = L.X + use;
+#if !HPK_RELOAD
     const bool cross = (xn ^ L.X) > 31u;
     L.d0 = cross ? L.d1 : L.d0;
     L.d1 = cross ? L.d2 : L.d1;
     L.d2 = cross ? d3 : L.d2;
+#endif
     L.X = xn;
     L.prog = a1 | park;
     if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
+#if HPK_RELOAD
+        const uint32_t* const pq = win32 + (L.X >> 5);
+        const uint32_t wp = __builtin_amdgcn_alignbit(pq[-1], pq[0], ~L.X);
+#else
         const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+#endif
         uint32_t s, len;
         bool eos;
         lo_decode(wp, lo, s, len, eos);
@@ -263,7 +282,7 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
                 L.o += 1;
             }
             L.X += len;
-            lit12_load(L, win32);
+            if (!HPK_RELOAD) lit12_load(L, win32);
         }
     }
 }
@@ -272,6 +291,14 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
 __device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
     if (L.st != HPK_OK) return L.st;
     return residual_status(L.Eb - L.X, __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X));
+}
+
+// The same for the step's window as the steps use it (HPK_RELOAD: read from the LDS window).
+__device__ __forceinline__ uint32_t lit12_status(const Lit12& L, const uint32_t* __restrict__ win32) {
+    if (!HPK_RELOAD) return lit12_status(L);
+    if (L.st != HPK_OK) return L.st;
+    const uint32_t* const q = win32 + (L.X >> 5);
+    return residual_status(L.Eb - L.X, __builtin_amdgcn_alignbit(q[-1], q[0], ~L.X));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1338,7 +1365,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     if (__any(fin)) {
                         if (fin && L.act) {
                             if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
-                            s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+                            s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L, win32) << 24);
                         }
                         const bool free_lane = fin || t >= kl;
                         const uint64_t fm = __ballot(free_lane);
@@ -1406,7 +1433,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     if (__any(fin)) {
                         if (fin && L.act) {
                             if (kAcc && L.accn) put32(s_out32, L.o, L.acc, L.oend, kStore);
-                            s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L) << 24);
+                            s_lenst[L.idx] = (kAcc ? L.cnt : L.o - L.o0) | (lit12_status(L, win32) << 24);
                         }
                         if (fin) {
                             if (nv) {
