@@ -56,14 +56,23 @@ static const uint8_t HPK_CODE_LEN[HPK_NSYM] = {
     30,                                                             /* EOS      */
 };
 
-// LUT2: the LUT's content in the layout of the bit-position step (decode v12, fields widened in
-// v20), chosen so the step clamps the bits left to 31 and needs one compare per code, and v_perm
-// gathers the two symbols:
-//   [7:0] sym0  [13:8] len0  [23:16] sym1  [29:24] len0+len1  [30] fewer than two  [31] none
-// a length field of a code the entry does not hold is 63 (never <= the clamped bits left).
+// LUT2: the LUT's content in the layout of the bit-position step (decode v12; fields re-packed in
+// v21), chosen so the checked step clamps the bits left to HPK_LUT2_CLAMP and needs one compare per
+// code, the unchecked body step (lit12_fast) reads the bits and codes an entry holds with one bfe
+// each, and v_perm / ds_write_b8_d16_hi take the two symbols where they are:
+//   [7:0] sym0  [11:8] len0  [15:12] bits held  [23:16] sym1  [27:24] len0+len1  [29:28] codes held
+//   [30] fewer than two  [31] none
+// a length field of a code the entry does not hold is 15 (never <= the clamped bits left); bits held
+// is 0 for an entry with no code (a 13..30-bit code or EOS starts here).
 #define HPK_LUT2_NOTTWO 0x40000000u  // e >= : fewer than two codes
-#define HPK_LUT2_NONE 0xC0000000u    // e >= : no code (a 13..30-bit code or EOS starts here)
-#define HPK_LUT2_MISSING 63u         // the length field of a code the entry does not hold
+#define HPK_LUT2_NONE 0x80000000u    // e >= : no code (a 13..30-bit code or EOS starts here)
+#define HPK_LUT2_MISSING 15u         // the length field of a code the entry does not hold
+#define HPK_LUT2_CLAMP 14u           // bits left are clamped to this before the length compares
+#define HPK_L2_LEN0(e) (((e) >> 8) & 15u)
+#define HPK_L2_HELD(e) (((e) >> 12) & 15u)
+#define HPK_L2_LEN01(e) (((e) >> 24) & 15u)
+#define HPK_L2_CODES(e) (((e) >> 28) & 3u)
+#define HPK_L2_TWO(e) (((e) >> 29) & 1u)
 
 struct hpk_tables {
     uint32_t code[HPK_NSYM];   // right-aligned canonical code
@@ -134,7 +143,7 @@ static inline int hpk_build_tables(hpk_tables* t) {
         }
         if (s0 < 0) {
             t->lut[v] = 0;
-            t->lut2[v] = HPK_LUT2_NONE | (HPK_LUT2_MISSING << 8) | (HPK_LUT2_MISSING << 24);
+            t->lut2[v] = 0xC0000000u | (HPK_LUT2_MISSING << 8) | (HPK_LUT2_MISSING << 24);
             continue;
         }
         uint32_t w1 = w << l0;
@@ -147,10 +156,10 @@ static inline int hpk_build_tables(hpk_tables* t) {
         uint32_t e2 = (uint32_t)s0 | ((uint32_t)l0 << 8);
         if (s1 >= 0) {
             e |= ((uint32_t)s1 << 8) | ((uint32_t)(l0 + l1) << 21) | (2u << 26);
-            e2 |= ((uint32_t)s1 << 16) | ((uint32_t)(l0 + l1) << 24);
+            e2 |= ((uint32_t)s1 << 16) | ((uint32_t)(l0 + l1) << 24) | ((uint32_t)(l0 + l1) << 12) | (2u << 28);
         } else {
             e |= ((uint32_t)l0 << 21) | (1u << 26);
-            e2 |= (HPK_LUT2_MISSING << 24) | HPK_LUT2_NOTTWO;
+            e2 |= (HPK_LUT2_MISSING << 24) | ((uint32_t)l0 << 12) | (1u << 28) | HPK_LUT2_NOTTWO;
         }
         t->lut[v] = e;
         t->lut2[v] = e2;

@@ -28,6 +28,9 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_FAST
+#define HPK_FAST 0  // 1: body steps without fit tests + a checked tail pass (measured slower)
+#endif
 #ifndef HPK_RELOAD
 // 1: lane steps read the window's two dwords each step instead of shifting a 3-dword register window
 // (5 fewer VALU per step, but the read sits on the step's dependency chain: config 2 46.2 vs 45.6 us,
@@ -121,8 +124,8 @@ __device__ __forceinline__ void wc_adv(WinCur& c, uint32_t n, uint32_t d3) {
 // inside the literal; returns the bits they use.
 __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
     // a length field the entry does not hold is 63, past any clamped rem (and t1 >= l1: ok2 => ok1)
-    const uint32_t rc = min(rem, 31u);
-    const uint32_t l1 = (e >> 8) & 63u, t1 = (e >> 24) & 63u;
+    const uint32_t rc = min(rem, HPK_LUT2_CLAMP);
+    const uint32_t l1 = HPK_L2_LEN0(e), t1 = HPK_L2_LEN01(e);
     ok1 = l1 <= rc;
     ok2 = t1 <= rc;
     return ok2 ? t1 : (ok1 ? l1 : 0u);
@@ -287,6 +290,66 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     }
 }
 
+// The body step (v21, kFast): the same two lookups with no per-code fit test. A step commits only
+// when every code its two entries hold ends inside the literal (X + held1 + held2 <= Eb: one compare
+// for the step); otherwise it changes nothing, and the literal's last bits are left to the checked
+// step (lit12_step) in the tail pass after the lane loop, so the step's stores and advances need no
+// fit flags, only the held counts. prog = false at a step that stops: it overran the literal's end,
+// or no code of <= 12 bits starts here and fewer than 13 bits are left. A stopped walk is a fixed
+// point (the same step stops again), so a lane can keep stepping until its wave leaves the loop.
+// Stores go in an order that leaves no byte outside the step's output: a slot an entry does not
+// fill is written first and then overwritten (sym1 at o + two, then sym0 at o), a second entry with
+// no code writes to the dummy slot, and a step that stops writes only there. A park (a longer code
+// with >= 13 bits left) lets the first entry's bytes land on o, where the park's own byte goes; an
+// error there (EOS, or a code running past the end) leaves them in the literal's own slack: it has
+// >= 13 unconsumed bits, so its decoded length is >= 2 below the bound (huffman.rs:95-161).
+__device__ __forceinline__ void lit12_fast(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, uint32_t dmy) {
+    const uint32_t d3 = win32[(L.X >> 5) + 2];  // the dword after d2, in case this step crosses one
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+    const uint32_t h1 = HPK_L2_HELD(e1);
+    const uint32_t e2 = lut[(w << h1) >> (32 - HPK_LUT_BITS)];  // (no code: h1 = 0, e2 = e1)
+    const uint32_t xn = L.X + h1 + HPK_L2_HELD(e2);
+    const bool none2 = e2 >= HPK_LUT2_NONE;
+    const bool park = none2 & (xn + (uint32_t)HPK_LUT_BITS < L.Eb);  // >= 13 bits left at xn
+    // a step at a longer code (no code in e1: xn = X) needs >= 13 bits; otherwise its codes must fit
+    const bool stop = xn + (e1 >> 31) * (uint32_t)(HPK_LUT_BITS + 1) > L.Eb;
+    const uint32_t n1 = HPK_L2_CODES(e1);
+    const uint32_t b1 = stop ? dmy : L.o;
+    out8[b1 + HPK_L2_TWO(e1)] = (uint8_t)(e1 >> 16);
+    out8[b1] = (uint8_t)e1;
+    const uint32_t b2 = none2 ? dmy : b1 + n1;
+    out8[b2 + HPK_L2_TWO(e2)] = (uint8_t)(e2 >> 16);
+    out8[b2] = (uint8_t)e2;
+    L.o = stop ? L.o : L.o + n1 + HPK_L2_CODES(e2);
+    const uint32_t xc = stop ? L.X : xn;
+    const bool cross = (xc ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xc;
+    L.prog = !stop;
+    if (park) {  // a 13..30-bit code or EOS with more than 12 bits left: one leading-ones lookup
+        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+        uint32_t s, len;
+        bool eos;
+        lo_decode(wp, lo, s, len, eos);
+        if (len > L.Eb - L.X) {  // nothing fits in what is left: huffman.rs:128-134
+            L.st = HPK_PADDING_TOO_LARGE;
+            L.Eb = L.X;
+        } else if (eos) {  // huffman.rs:112-116
+            L.st = HPK_EOS_IN_STRING;
+            L.Eb = L.X;
+        } else {
+            out8[L.o] = (uint8_t)s;
+            L.o += 1;
+            L.X += len;
+            lit12_load(L, win32);
+        }
+    }
+}
+
 // Final status of a literal whose walk has stopped; a status set by the walk wins.
 __device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
     if (L.st != HPK_OK) return L.st;
@@ -343,13 +406,13 @@ __device__ __forceinline__ uint32_t seg_walk(const uint32_t* __restrict__ win32,
         lut12(e1, rem, a1, a2);
         uint32_t adv = 0;
         if (a1) {
-            const uint32_t l1 = (e1 >> 8) & 63u;
+            const uint32_t l1 = HPK_L2_LEN0(e1);
             if (kWrite) put8(out8, o + cnt, e1, oend, kStore);
             cnt += 1;
             if (a2 && pos + l1 < e) {  // the second code also starts inside the segment
                 if (kWrite) put8(out8, o + cnt, e1 >> 16, oend, kStore);
                 cnt += 1;
-                adv = (e1 >> 24) & 63u;
+                adv = HPK_L2_LEN01(e1);
             } else {
                 adv = l1;
             }
@@ -428,13 +491,13 @@ __device__ __forceinline__ SegWalk seg_record(const uint32_t* __restrict__ win32
         bool a1, a2;
         lut12(e1, rem, a1, a2);
         if (a1) {
-            const uint32_t p2 = pos + ((e1 >> 8) & 63u);
+            const uint32_t p2 = pos + (HPK_L2_LEN0(e1));
             r.cnt += 1;
             r.pos = p2;
             if (a2 && p2 < e) {  // the second code also starts inside the segment
                 if (join(p2)) break;
                 r.cnt += 1;
-                r.pos = pos + ((e1 >> 24) & 63u);
+                r.pos = pos + (HPK_L2_LEN01(e1));
             }
             run = r.pos < e;
         } else if (e1 >= HPK_LUT2_NONE && rem > (uint32_t)HPK_LUT_BITS) {
@@ -506,8 +569,8 @@ __device__ __forceinline__ void long_decode(const uint32_t* __restrict__ win32, 
             lut12(e1, rem, a1, a2);
             uint32_t adv = 0;
             if (a1) {
-                const uint32_t l1 = (e1 >> 8) & 63u;
-                adv = (a2 && p + l1 < s0) ? (e1 >> 24) & 63u : l1;
+                const uint32_t l1 = HPK_L2_LEN0(e1);
+                adv = (a2 && p + l1 < s0) ? HPK_L2_LEN01(e1) : l1;
             } else if (e1 >= HPK_LUT2_NONE && rem > (uint32_t)HPK_LUT_BITS) {
                 uint32_t sy, len;
                 bool eos;
@@ -627,7 +690,7 @@ __device__ __forceinline__ void walk2(const uint32_t* __restrict__ win32, const 
         const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
         const uint32_t kk = __clz(~w);
         const uint32_t el = lo_tab[min(kk, (uint32_t)HPK_LO_RUNS - 1u) * 32u + ((w << ((kk + 1u) & 31u)) >> 27)];
-        const uint32_t l1 = (e1 >> 8) & 63u, t1 = (e1 >> 24) & 63u;
+        const uint32_t l1 = HPK_L2_LEN0(e1), t1 = HPK_L2_LEN01(e1);
         const bool ok1 = (e1 < HPK_LUT2_NONE) & (l1 <= rem);
         const uint32_t i2 = i0 + l1;
         bool ok2 = ok1 & (e1 < HPK_LUT2_NOTTWO) & (t1 <= rem) & (s0 + i2 < e);  // the second code starts in the segment
@@ -878,6 +941,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
     constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : (kPredSt ? kPred : kDword));
+    // v21: body steps without fit tests, the literals' last bits in a checked tail pass (lit12_fast)
+    constexpr bool kFast = HPK_FAST && kStore == kPred && !kAcc && kLook == 2 && !HPK_RELOAD && !kDefer;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
     constexpr int kImg = kStore == kPred ? kO - 256 : kO;
     const uint32_t dmy = (uint32_t)kImg + (threadIdx.x & 63u) * 4u;
@@ -1424,7 +1489,35 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 const uint32_t t2 = 2u * G::kBlock - 1u - t1;
                 bool nv = t2 < kl;  // a second literal is waiting in N
                 load(N, t2);
-                for (;;) {
+                if (kFast) {
+                    // body steps until every lane's literals have stopped (the first one's stopped state
+                    // moves to N when the second starts), then both tails with the checked step, the two
+                    // lanes' walks interleaved
+                    for (;;) {
+    #pragma unroll
+                        for (int s = 0; s < kRefillN; ++s) lit12_fast(L, win32, s_lut, s_lo, s_out, dmy);
+                        if (kMode == 3) n_steps += kRefillN;
+                        const bool fin = !L.prog;
+                        if (__any(fin)) {
+                            const bool sw = fin & nv;
+                            if (sw) {
+                                const Lit12 T = L;
+                                L = N;
+                                N = T;
+                                nv = false;
+                            }
+                            if (!__any(!fin | sw)) break;
+                        }
+                    }
+                    for (;;) {
+                        lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
+                        lit12_step<kStore, kLook, kAcc>(N, win32, s_lut, s_lo, s_out, dmy);
+                        if (!__any(L.prog | N.prog)) break;
+                    }
+                    if (L.act) s_lenst[L.idx] = (L.o - L.o0) | (lit12_status(L) << 24);
+                    if (N.act) s_lenst[N.idx] = (N.o - N.o0) | (lit12_status(N) << 24);
+                }
+                for (; !kFast;) {
     #pragma unroll
                     for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
                     if (kMode == 3) n_steps += kRefillN;
