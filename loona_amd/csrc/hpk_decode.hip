@@ -40,7 +40,10 @@ using namespace hpkdec;
 // window, a 77 KiB output image and a 2048-entry longest-first queue, plus the 16 KiB two-symbol
 // table; two lookups per step, lanes check for a finished literal every 2 steps, static snake
 // schedule, byte stores into the image (bench/kvariants: profiles/r01/kvariants_v1[23]*.jsonl).
-constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2, kChunk = 64, kLook = 2, kSched = 1;
+#ifndef HPK_REFILLN
+#define HPK_REFILLN 2  // lane steps between two finish checks
+#endif
+constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = HPK_REFILLN, kChunk = 64, kLook = 2, kSched = 1;
 constexpr bool kAcc = false;
 constexpr int kCoop = 0;  // (v16: literals of >= 224 encoded bytes one wave each; v19: hpk_decode_long)
 #ifndef HPK_LONGK
