@@ -141,6 +141,11 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
     }
 }
 
+#ifndef HPK_ENC_PAIR
+#define HPK_ENC_PAIR 0  // 1: pass 2 ORs two codes at once where the whole wave can (measured slower)
+#endif
+constexpr bool kPair = HPK_ENC_PAIR;
+
 template <int kEB, int kEO, int kEQ, int kEBytes = 32, int kProf = 0>  // kEBytes: input bytes per thread per tile (16 or 32)
 // (at least 4 waves per SIMD: two 512-thread workgroups per CU fit only under 128 VGPRs)
 __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
@@ -388,36 +393,56 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
                 uint2 tb[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) tb[j] = S.tab[((j < 4 ? lo8 : hi8) >> (8 * (j & 3))) & 0xFFu];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint2 cl = tb[j];
-                    if ((bm8 >> j) & 1u) {  // a run starts here: close the previous one
-                        if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
-                        if (!ph) S.bits[lj] = dq * 32u + n - qs;
-                        const uint32_t x = xt + 8u * g + (uint32_t)j;
-                        if (nx > x) {
-                            ++lj;
-                            qs = nq;
-                        } else {
-                            while (S.ioff[lj + 1] <= x) ++lj;  // (empty literals between: bits stay 0)
-                            qs = S.ooff[lj] * 8u;
-                        }
-                        ph = lj >= k;  // (k: the tile's literals) the tile's end: the rest is a phantom
-                        qs = ph ? qph : qs;
-                        nq = S.ooff[lj + 1u] * 8u;
-                        nx = S.ioff[lj + 2u];
-                        dq = qs >> 5;
-                        n = qs & 31u;
-                        acc = 0;
+                // a run starts at byte j: close the previous one
+                auto start = [&](int j) {
+                    if (n) atomicOr(&S.img[dq], (uint32_t)(acc << (32u - n)));
+                    if (!ph) S.bits[lj] = dq * 32u + n - qs;
+                    const uint32_t x = xt + 8u * g + (uint32_t)j;
+                    if (nx > x) {
+                        ++lj;
+                        qs = nq;
+                    } else {
+                        while (S.ioff[lj + 1] <= x) ++lj;  // (empty literals between: bits stay 0)
+                        qs = S.ooff[lj] * 8u;
                     }
+                    ph = lj >= k;  // (k: the tile's literals) the tile's end: the rest is a phantom
+                    qs = ph ? qph : qs;
+                    nq = S.ooff[lj + 1u] * 8u;
+                    nx = S.ioff[lj + 2u];
+                    dq = qs >> 5;
+                    n = qs & 31u;
+                    acc = 0;
+                };
+                // one code: the current dword's bits so far — all of them once it is complete — ORed
+                // in (a prefix ORs nothing the complete dword does not)
+                auto put = [&](uint2 cl) {
                     acc = (acc << cl.y) | cl.x;
                     n += cl.y;  // 5 <= n < 62
-                    // the current dword's bits so far — all of them once it is complete — ORed in
-                    // every byte (a prefix ORs nothing the complete dword does not)
                     atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
                     const bool full = n >= 32u;
                     dq += full ? 1u : 0u;
                     n &= 31u;
+                };
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    const uint2 c0 = tb[j], c1 = tb[j + 1];
+                    if ((bm8 >> j) & 1u) start(j);
+                    // v5: two codes per OR when no run starts at the second byte and the two codes fit
+                    // the dword's room (n < 32 before, < 64 after: at most one dword completes); the
+                    // test is wave-uniform, so a wave takes one path or the other, never both
+                    const bool one = ((bm8 >> (j + 1)) & 1u) | (c0.y + c1.y > 32u);
+                    if (!kPair || __any(one)) {
+                        put(c0);
+                        if ((bm8 >> (j + 1)) & 1u) start(j + 1);
+                        put(c1);
+                    } else {
+                        acc = (((acc << c0.y) | c0.x) << c1.y) | c1.x;
+                        n += c0.y + c1.y;
+                        atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
+                        const bool full = n >= 32u;
+                        dq += full ? 1u : 0u;
+                        n &= 31u;
+                    }
                 }
             }
             if (any && !ph) {
