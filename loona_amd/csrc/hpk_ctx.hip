@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.20 gfx950 decode v20 (alignbit step, two lookups per step with clamped 6-bit LUT2 lengths, unconditional byte stores, static snake schedule, equal-size fills, LDS image; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
+#define HPK_VERSION "hpk 0.21 gfx950 decode v21 (alignbit step, two lookups per step with clamped 4-bit LUT2 lengths, unconditional byte stores, static snake schedule, equal-size fills, LDS image; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
 
 static thread_local std::string t_last_error;
 
