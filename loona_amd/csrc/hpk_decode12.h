@@ -28,6 +28,9 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_LATE_FIN
+#define HPK_LATE_FIN 1  // 0: a finished lane literal's length and status are made in the finish round (v21)
+#endif
 #ifndef HPK_FAST
 #define HPK_FAST 0  // 1: body steps without fit tests + a checked tail pass (measured slower)
 #endif
@@ -943,6 +946,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : (kPredSt ? kPred : kDword));
     // v21: body steps without fit tests, the literals' last bits in a checked tail pass (lit12_fast)
     constexpr bool kFast = HPK_FAST && kStore == kPred && !kAcc && kLook == 2 && !HPK_RELOAD && !kDefer;
+    // v22: lengths and statuses of the lane literals made after the lane loop (HPK_LATE_FIN)
+    constexpr bool kLate = HPK_LATE_FIN && !kFast && kStore == kPred && !kAcc && !HPK_RELOAD && !kDefer && !kSpread;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
     constexpr int kImg = kStore == kPred ? kO - 256 : kO;
     const uint32_t dmy = (uint32_t)kImg + (threadIdx.x & 63u) * 4u;
@@ -1517,7 +1522,40 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     if (L.act) s_lenst[L.idx] = (L.o - L.o0) | (lit12_status(L) << 24);
                     if (N.act) s_lenst[N.idx] = (N.o - N.o0) | (lit12_status(N) << 24);
                 }
-                for (; !kFast;) {
+                if (kLate) {
+                    // v22: a lane's first literal that ends leaves only its end state (bit and output
+                    // positions, walk status) in three registers as the second one starts; lengths and
+                    // statuses (the padding check) are made once per lane after the loop, not in every
+                    // finish round a wave takes (a round ran the check whenever any of its lanes finished)
+                    uint32_t sX = 0, sO = 0, sSt = 0;
+                    bool s1 = false;  // the first literal's end state is saved
+                    for (;;) {
+    #pragma unroll
+                        for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
+                        if (kMode == 3) n_steps += kRefillN;
+                        const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
+                        if (__any(fin)) {
+                            const bool sw = fin & nv;
+                            if (sw) {
+                                sX = L.X;
+                                sO = L.o;
+                                sSt = L.st;
+                                s1 = L.act;
+                                L = N;
+                                nv = false;
+                            }
+                            if (!__any(!fin | sw)) break;
+                        }
+                    }
+                    if (s1) {
+                        const uint2 e = lq[t1];
+                        const uint32_t Eb = (e.x & 0xFFFFu) * 8u + 31u + (e.x >> 16) * 8u;
+                        const uint32_t st = sSt != HPK_OK ? sSt : residual_status(Eb - sX, win_at(win32, sX - 31u));
+                        s_lenst[e.y & 0xFFFu] = (sO - ((e.y >> 12) & 0x1FFFFu)) | (st << 24);
+                    }
+                    if (L.act) s_lenst[L.idx] = (L.o - L.o0) | (lit12_status(L) << 24);
+                }
+                for (; !kFast && !kLate;) {
     #pragma unroll
                     for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
                     if (kMode == 3) n_steps += kRefillN;
