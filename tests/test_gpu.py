@@ -135,6 +135,57 @@ def test_long_literals(codec):
     compare_batches(gpu_decode(codec, blob, off), oracle_decode_batch(blob, off), "long literals")
 
 
+def test_split_long_literals(codec):
+    """v22: literals of 1.5-6 KiB encoded (left to the long-literal phase) are decoded as two pieces by
+    two lanes and joined where their walks meet. Text and random bytes (long codes: the pieces meet
+    late), an EOS before, near and after the split byte at every offset class mod 64 bits, bad and
+    too-long padding, a run of ones from the middle on (the second piece starts in an EOS), literals
+    just below and above the split range, at exact-bound regions on an unaligned base with guard
+    bytes. Bit-exact (lengths, statuses, bytes) against the oracle."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(2207)
+    text = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;,/.:ABCDEFGHIJ ", np.uint8)
+    lits = []
+    for n in rng.integers(1800, 8200, size=40):  # text: 1.3-6 KB encoded
+        lits.append(huffman_encode(rng.choice(text, int(n)).tobytes()))
+    for n in rng.integers(700, 2600, size=40):  # uniform bytes: ~2.3x, 1.6-6 KB encoded
+        lits.append(huffman_encode(rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()))
+    for n in rng.integers(1536, 6200, size=20):  # random bits: padding errors, false codes
+        lits.append(rng.integers(0, 256, int(n), dtype=np.uint8).tobytes())
+    eos = (1 << 30) - 1
+    for frac in (0.1, 0.45, 0.49, 0.5, 0.51, 0.55, 0.9):
+        for k in range(0, 64, 7):  # EOS at a fraction of a ~2.4 KB literal, offset classes mod 64
+            m = int(2800 * frac) + k
+            body = huffman_encode(b"x" * m)
+            bits = int.from_bytes(body, "big") >> (len(body) * 8 - m * 7)  # 'x' is 7 bits
+            after = huffman_encode(b"y" * (2800 - m))
+            abits = int.from_bytes(after, "big")
+            tot = m * 7 + 30 + len(after) * 8
+            v = (((bits << 30) | eos) << (len(after) * 8)) | abits
+            pad = (-tot) % 8
+            lits.append(((v << pad) | ((1 << pad) - 1)).to_bytes((tot + pad) // 8, "big"))
+    for k in range(16):  # bad padding / too much padding at the end
+        body = bytearray(huffman_encode(b"content-security-policy: default-src 'self'" * (60 + k)))
+        body[-1] &= 0xF0
+        lits.append(bytes(body))
+        lits.append(huffman_encode(b"z" * (2000 + 37 * k)) + b"\xff")
+    half = huffman_encode(rng.choice(text, 2500).tobytes())
+    lits.append(half + b"\xff" * len(half))  # ones from the middle on: EOS where the text ends
+    lits.append(b"\xff" * 2000)
+    for n in (1535, 1536, 1537, 6144, 6145):  # the split range's edges (encoded bytes)
+        s = huffman_encode(rng.choice(text, n * 2).tobytes())[:n]
+        lits.append(s)
+        lits.append(rng.integers(0, 256, 40, dtype=np.uint8).tobytes())  # short ones between
+    blob, off = pack(lits)
+    ref = oracle_decode_batch(blob, off)
+    compare_batches(gpu_decode(codec, blob, off), ref, "split literals")
+    bound = [int(off[i + 1] - off[i]) * 8 // 5 for i in range(len(off) - 1)]
+    got, guard = _decode_regions(codec, blob, off, bound, shift=3)
+    compare_batches(got, ref, "split literals, exact-bound regions at +3")
+    assert (guard == 0xAB).all()
+
+
 def _decode_regions(codec, blob, off, caps, shift=0, guard=64):
     """Decode into caller-chosen region sizes `caps` (back to back), the output buffer surrounded
     by guard bytes; returns (out, out_off, out_len, status) over the regions and the guard bytes."""
