@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.21 gfx950 decode v21 (alignbit step, two lookups per step with clamped 4-bit LUT2 lengths, unconditional byte stores, static snake schedule, equal-size fills, LDS image; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
+#define HPK_VERSION "hpk 0.22 gfx950 decode v22 (alignbit step, two lookups per step with clamped 4-bit LUT2 lengths, unconditional byte stores, static snake schedule with lengths and statuses made after the lane loop, equal-size fills, LDS image; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
 
 static thread_local std::string t_last_error;
 
@@ -74,7 +74,7 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     return c;
 }
 
-int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list) {
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list) {
     int j = -1;
     for (int k = 0; k < hpk_ctx::kLongSlots; ++k)
         if (c->long_list[k] && c->long_stream[k] == c->stream) j = k;
@@ -88,12 +88,12 @@ int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list) {
         }
         c->long_stream[j] = c->stream;
     }
-    if (c->long_list_cap[j] < n || !c->long_list[j]) {  // grow: the old list may still be in use
+    if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
         HIP_TRY(hipStreamSynchronize(c->stream));
         (void)hipFree(c->long_list[j]);
         c->long_list[j] = nullptr;
         c->long_list_cap[j] = 0;
-        const size_t cap = n + (n >> 2) + 1024;
+        const size_t cap = (size_t)n + (n >> 2) + 1024;
         HIP_TRY(hipMalloc(&c->long_list[j], cap * sizeof(uint32_t)));
         c->long_list_cap[j] = cap;
     }

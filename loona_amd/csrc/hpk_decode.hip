@@ -84,9 +84,6 @@ static int g_debug_mode = -1;
 static unsigned long long* g_dbg = nullptr;
 static size_t g_dbg_n = 0;
 
-extern "C" int hpk_debug_split_stat(unsigned long long* host4) {  // (cumulative) met, A EOS, rest decoded, bits
-    return hipMemcpyFromSymbol(host4, HIP_SYMBOL(g_split_stat), 4 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
 extern "C" int hpk_debug_check(unsigned long long* host8) {
     return hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_chk), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
 }
@@ -120,27 +117,19 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
+    uint32_t* ll = nullptr;
+    if (int rc = hpk_long_list(c, b.n, &ll)) return rc;
+    a.long_list = ll;
+    a.long_min = HPK_LONG_MIN;
+    a.long_big = HPK_LONG_BIG;
+#ifdef HPK_DIAG
+    if (const char* lm = getenv("HPK_LONG_MIN")) a.long_min = (uint32_t)atoi(lm);
+    if (const char* lb = getenv("HPK_LONG_BIG")) a.long_big = (uint32_t)atoi(lb);
+#endif
     // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
-    // the long list: two entries per literal (a split literal lists its two pieces), then the
-    // workgroups' split pools
-    uint32_t* ll = nullptr;
-    if (int rc = hpk_long_list(c, 2 * (size_t)b.n + (size_t)blocks * HPK_SPLIT_K, &ll)) return rc;
-    a.long_list = ll;
-    a.long_min = HPK_LONG_MIN;
-    a.long_big = HPK_LONG_BIG;
-    a.split_pool = ll + 2 * (size_t)b.n;
-    // (split list entries carry a pool index below 2^30 and the pieces' length and status stores are
-    // dropped by offset: small enough batches only)
-    a.split_min = (HPK_SPLIT && b.n < (1u << 29)) ? HPK_SPLIT_MIN : 0xFFFFFFFFu;
-    a.split_max = HPK_SPLIT_MAX;
-#ifdef HPK_DIAG
-    if (const char* lm = getenv("HPK_LONG_MIN")) a.long_min = (uint32_t)atoi(lm);
-    if (const char* lb = getenv("HPK_LONG_BIG")) a.long_big = (uint32_t)atoi(lb);
-    if (const char* sm = getenv("HPK_SPLIT_MIN")) a.split_min = (uint32_t)atoi(sm);
-#endif
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
 #ifdef HPK_DIAG
     if (g_debug_mode < 0) {

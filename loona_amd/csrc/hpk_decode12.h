@@ -1107,25 +1107,11 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
     // kLongK: long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
-    // (list positions [2 BA, 2 BB): a split literal, of [split_min, split_max] bytes, lists its two
-    // pieces at the front, as pool index k | bit 31 (| bit 30: the second piece), the pool entry
-    // holding its literal index; split_pool[blockIdx.x * HPK_SPLIT_K + k], k counted in s_ctr[11])
     auto leave = [&](uint32_t i, uint32_t nb) {
-        if (nb >= a.split_min && nb <= a.split_max) {
-            const uint32_t k = atomicAdd(&s_ctr[11], 1u);
-            if (k < (uint32_t)HPK_SPLIT_K) {
-                const uint32_t id = blockIdx.x * (uint32_t)HPK_SPLIT_K + k;
-                a.split_pool[id] = i;
-                const uint32_t p = 2u * BA + atomicAdd(&s_ctr[6], 2u);
-                a.long_list[p] = id | 0x80000000u;
-                a.long_list[p + 1u] = id | 0xC0000000u;
-                return;
-            }
-        }
         if (nb >= a.long_big)
-            a.long_list[2u * BA + atomicAdd(&s_ctr[6], 1u)] = i;
+            a.long_list[BA + atomicAdd(&s_ctr[6], 1u)] = i;
         else
-            a.long_list[2u * BB - 1u - atomicAdd(&s_ctr[7], 1u)] = i;
+            a.long_list[BB - 1u - atomicAdd(&s_ctr[7], 1u)] = i;
     };
     if (kLongK) {
         if (tid == 0) {
@@ -1133,7 +1119,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             s_ctr[7] = 0;
             s_ctr[8] = 0;
             s_ctr[9] = 0;
-            s_ctr[11] = 0;
         }
     }
 
@@ -1255,7 +1240,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[6] = 0;  // (this fill's entries are listed again below)
                     s_ctr[7] = 0;
-                    s_ctr[11] = 0;
                     s_ctr[10] = 0;
                 }
                 lds_barrier();
@@ -1279,7 +1263,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[6] = 0;
                     s_ctr[7] = 0;
-                    s_ctr[11] = 0;
                 }
                 continue;  // this fill again, from its setup (its prefetched offsets and window are still
                            // in the registers)
@@ -1665,12 +1648,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         lds_barrier();
         if (tid == 0) s_ctr[5] = 0;  // its claim counter
         __syncthreads();  // (every thread's list entries and stores are out)
-        static_assert(kW + kO >= 512 * (32 * 4 + HPK_LONG_OS) + 16 * HPK_SPLIT_K && G::kInOff % 16 == 0 && kW % 16 == 0,
-                      "long-phase LDS");
-        long_phase<512, 8, 32, kMode == 5 ? 1 : 0, G::kBlock>(
-            a, 2u * BA, 2u * BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + 512 * 32 * 4,
-            reinterpret_cast<uint4*>(s_q), s_lut, s_lo, s_ctr[11],
-            reinterpret_cast<uint4*>(s_in + 512 * (32 * 4 + HPK_LONG_OS)));
+        static_assert(kW + kO >= 512 * (32 * 4 + HPK_LONG_OS) && G::kInOff % 16 == 0 && kW % 16 == 0, "long-phase LDS");
+        long_phase<512, 8, 32, kMode == 5 ? 1 : 0, G::kBlock>(a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5],
+                                                              reinterpret_cast<uint32_t*>(s_in), s_in + 512 * 32 * 4,
+                                                              reinterpret_cast<uint4*>(s_q), s_lut, s_lo);
     }
 }
 

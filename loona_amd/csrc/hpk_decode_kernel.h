@@ -7,19 +7,6 @@
 
 #include "hpk_device.h"
 
-// Split long literals (v22, hpk_long.h): a literal of [HPK_SPLIT_MIN, HPK_SPLIT_MAX] encoded bytes
-// left to the long-literal phase is decoded as two pieces by two lanes, joined afterwards.
-#ifndef HPK_SPLIT
-#define HPK_SPLIT 1
-#endif
-#ifndef HPK_SPLIT_MIN
-#define HPK_SPLIT_MIN 1536
-#endif
-#ifndef HPK_SPLIT_MAX
-#define HPK_SPLIT_MAX 6144
-#endif
-#define HPK_SPLIT_K 256  // split literals per fill workgroup at most (its pool and LDS records)
-
 namespace hpkdec {
 
 // Tables in LDS (once per workgroup): T8 (256 B, symbols of the <= 8-bit codes) and the
@@ -50,10 +37,6 @@ struct DecodeArgs {
     // those of >= long_big bytes from the front, the others from the back
     uint32_t* long_list;
     uint32_t long_min, long_big;
-    // split long literals (hpk_long.h): fill workgroup g's literal indices of split literal k at
-    // split_pool[g * HPK_SPLIT_K + k]; literals of [split_min, split_max] encoded bytes are split
-    uint32_t* split_pool;
-    uint32_t split_min, split_max;
 };
 
 // Per-lane state of the literal being decoded.

@@ -48,7 +48,7 @@ struct hpk_ctx {
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on
 // first use; HPK_E_OK or an error code).
-int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list);
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list);
 
 // One batch call as the launchers see it: capacities clamped to HPK_MAX_OFFSET (offsets above
 // them are bad whatever the buffer size).

@@ -79,185 +79,6 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 #define HPK_LONG_OS 80  // output buffer bytes per lane (a multiple of 16; 80: 20-dword stride, 4-way bank aliasing instead of 96's 8-way, config 3 870 vs 883 us)
 #endif
 
-#ifdef HPK_DIAG
-__device__ unsigned long long g_split_stat[4];
-#endif
-
-// Split literals (v22). A long literal of [split_min, split_max] encoded bytes is decoded by two
-// lanes: piece A from its first bit to the middle byte S (a walk that stops where no code fits
-// before S, its output at the region's start), piece B from S to the end (its output at the region's
-// end minus its half's bound). B's walk starts at a byte boundary that is not in general a code
-// boundary, but Huffman walks fall into step within a few codes (config 3: 78 % within 64 bits, 95 %
-// within 128). Once every piece of the workgroup has ended, one lane per split literal walks on from
-// A's stop and from S at once, always advancing the one behind, until the two stand on the same bit
-// P: from P on both decode the same codes, so the literal is A's bytes up to P followed by B's bytes
-// from its code at P on. The wave moves B's bytes into place, the lane writes A's codes between its
-// stop and P, then the length and B's status (B's walk ended at the literal's end). An EOS in A
-// before S is the literal's status (huffman.rs:112-116) and ends it there; no meeting point within
-// kSyncBits past S, or a B walk that stopped before it (a false EOS or overrun while out of step):
-// the lane decodes the rest of the literal from A's stop, code by code (lit_bytes_to's semantics).
-template <int kBlock>
-__device__ __forceinline__ void split_join(const DecodeArgs& a, uint32_t nsplit, uint4* s_rec, const uint16_t* s_lo,
-                                           __amdgpu_buffer_rsrc_t r_out, uint32_t in_end, uint32_t* s_stage) {
-    constexpr uint32_t kSyncBits = 2048;  // how far past the split byte the walks may run apart
-    constexpr uint32_t kSt = 20;          // staged dwords per split literal (17 used)
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t ns = min(nsplit, (uint32_t)HPK_SPLIT_K);
-    __syncthreads();  // every piece has ended: records in LDS, output in memory (release / acquire)
-    const uint32_t* gin = reinterpret_cast<const uint32_t*>(a.in_base);
-    const uint32_t last = in_end ? (in_end - 1u) >> 2 : 0u;  // last dword holding a batch byte
-    // the 32 bits at bit r of the bytes from in_base byte b0 on (MSB first), from global memory
-    auto bits_at = [&](uint32_t b0, uint32_t r) -> uint32_t {
-        const uint32_t t = r + (b0 & 3u) * 8u;
-        const uint32_t q = (b0 >> 2) + (t >> 5);
-        const uint64_t w = ((uint64_t)__builtin_bswap32(gin[min(q, last)]) << 32) | __builtin_bswap32(gin[min(q + 1u, last)]);
-        return (uint32_t)((w << (t & 31u)) >> 32);
-    };
-    struct Sp {
-        uint32_t i, p0, p1, q0, q1, sm, b0, endb, sb, pA, cA, stA, pBe, lenB, stB, bB;
-    };
-    auto split_at = [&](uint32_t k) {
-        Sp z;
-        z.i = a.split_pool[blockIdx.x * (uint32_t)HPK_SPLIT_K + k];
-        z.p0 = a.in_off[z.i];
-        z.p1 = a.in_off[z.i + 1];
-        z.q0 = a.out_off[z.i] + a.out_mis;
-        z.q1 = a.out_off[z.i + 1] + a.out_mis;
-        z.sm = z.p0 + ((z.p1 - z.p0) >> 1);
-        z.b0 = z.p0 + a.in_mis;
-        z.endb = (z.p1 - z.p0) * 8u;  // bit positions from the literal's start
-        z.sb = (z.sm - z.p0) * 8u;
-        const uint4 rc = s_rec[k];
-        z.pA = z.sb - rc.x;
-        z.cA = rc.y & 0xFFFFFFu;
-        z.stA = rc.y >> 24;
-        z.pBe = z.endb - rc.z;
-        z.lenB = rc.w & 0xFFFFFFu;
-        z.stB = rc.w >> 24;
-        z.bB = z.q1 - ((z.p1 - z.sm) * 8u) / 5u;  // B's output
-        return z;
-    };
-    // 1. one lane per split literal: the meeting point, walking both pieces' codes over 68 staged
-    // bytes around the split byte (in LDS; global memory past them). Result in s_res: mode (0: met at
-    // pa with A's count ca and B's cb; 1: A ended with an EOS; 2: decode the rest from A's stop),
-    // pa, ca, cb.
-    uint4* s_res = reinterpret_cast<uint4*>(s_stage + HPK_SPLIT_K * kSt);
-    if (tid < ns) {
-        const Sp z = split_at(tid);
-        uint32_t* st = s_stage + tid * kSt;
-        const uint32_t s0 = z.sm + a.in_mis - 8u;  // (a split literal has >= 8 bytes before sm)
-#pragma unroll
-        for (uint32_t j = 0; j < 17u; ++j) st[j] = __builtin_bswap32(gin[min((s0 >> 2) + j, last)]);
-        const uint32_t r0 = z.sb - 64u - (s0 & 3u) * 8u;  // the literal bit at staged bit 0
-        auto bits = [&](uint32_t r) -> uint32_t {
-            const uint32_t t = r - r0;
-            if (t < 15u * 32u) {
-                const uint64_t w = ((uint64_t)st[t >> 5] << 32) | st[(t >> 5) + 1u];
-                return (uint32_t)((w << (t & 31u)) >> 32);
-            }
-            return bits_at(z.b0, r);
-        };
-        uint32_t mode = 2, pa = z.pA, ca = z.cA, cb = 0;
-        if (z.stA == HPK_EOS_IN_STRING) {
-            mode = 1;
-        } else {
-            uint32_t pb = z.sb;
-            for (uint32_t it = 0; it < 2u * kSyncBits; ++it) {
-                if (pa == pb) {
-                    mode = 0;
-                    break;
-                }
-                if (pa > z.sb + kSyncBits) break;
-                const bool ta = pa < pb;
-                if (!ta && pb >= z.pBe) break;  // B's walk stopped here
-                const uint32_t p = ta ? pa : pb;
-                uint32_t sy, len;
-                bool eos;
-                lo_decode(bits(p), s_lo, sy, len, eos);
-                if (eos || len > z.endb - p) break;
-                pa += ta ? len : 0u;
-                ca += ta ? 1u : 0u;
-                pb += ta ? 0u : len;
-                cb += ta ? 0u : 1u;
-            }
-        }
-        s_res[tid] = make_uint4(mode, pa, ca, cb);
-#ifdef HPK_DIAG
-        atomicAdd(&g_split_stat[mode], 1ull);  // diagnostic build: join outcomes, meet distance
-        if (mode == 0) atomicAdd(&g_split_stat[3], (unsigned long long)(pa - z.sb));
-#endif
-    }
-    __syncthreads();
-    // 2. one wave per split literal that met: B's bytes [cb, lenB) to follow A's ca — a byte move,
-    // 1 KiB per round, every round read whole before it is stored, rounds in the move's direction
-    for (uint32_t k = wv; k < ns; k += (uint32_t)kBlock / 64u) {  // wave-uniform
-        const uint4 r = s_res[k];
-        if (r.x != 0u) continue;
-        const Sp z = split_at(k);
-        const uint32_t n = z.lenB - r.w, src = z.bB + r.w, dst = z.q0 + r.z;
-        const uint32_t rounds = (n + 1023u) >> 10;
-        for (uint32_t q = 0; q < rounds; ++q) {
-            const uint32_t c = (dst <= src ? q : rounds - 1u - q) * 1024u + lane * 16u;
-            uint32_t v[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                v[j] = c + j < n ? __builtin_amdgcn_raw_buffer_load_b8(r_out, src + c + j, 0, 0) : 0u;
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (c + j < n) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[j], r_out, dst + c + j, 0, 0);
-        }
-    }
-    __syncthreads();  // (the moves have read B's bytes before A's are written over them)
-    // 3. one lane per split literal: A's codes from its stop up to the meeting point (or, with no
-    // meeting point, to the literal's end: lit_bytes_to's semantics), then length and status
-    if (tid < ns) {
-        const Sp z = split_at(tid);
-        const uint4 r = s_res[tid];
-        const uint32_t* st = s_stage + tid * kSt;
-        const uint32_t s0 = z.sm + a.in_mis - 8u;
-        const uint32_t r0 = z.sb - 64u - (s0 & 3u) * 8u;
-        auto bits = [&](uint32_t rb) -> uint32_t {
-            const uint32_t t = rb - r0;
-            if (t < 15u * 32u) {
-                const uint64_t w = ((uint64_t)st[t >> 5] << 32) | st[(t >> 5) + 1u];
-                return (uint32_t)((w << (t & 31u)) >> 32);
-            }
-            return bits_at(z.b0, rb);
-        };
-        uint32_t olen = z.cA, ost = HPK_EOS_IN_STRING;
-        if (r.x != 1u) {
-#ifndef HPK_SPLIT_FAKE_REST
-#define HPK_SPLIT_FAKE_REST 0  // experiment only: 1 = the rest is not decoded (wrong output, timing the joins alone)
-#endif
-            const uint32_t stop = r.x == 0u ? r.y : (HPK_SPLIT_FAKE_REST ? z.pA : z.endb);
-            uint32_t p = z.pA, c = z.cA, stt = HPK_OK;
-            while (p < stop) {
-                const uint32_t w = bits(p);
-                uint32_t sy, len;
-                bool eos;
-                lo_decode(w, s_lo, sy, len, eos);
-                const uint32_t rb = z.endb - p;
-                if (len > rb) {  // huffman.rs:128-160
-                    stt = rb > 7u ? HPK_PADDING_TOO_LARGE
-                                  : ((w | (0xFFFFFFFFu >> rb)) != 0xFFFFFFFFu ? HPK_INVALID_PADDING : HPK_OK);
-                    break;
-                }
-                if (eos) {
-                    stt = HPK_EOS_IN_STRING;
-                    break;
-                }
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sy, r_out, z.q0 + c, 0, 0);
-                c += 1;
-                p += len;
-            }
-            olen = r.x == 0u ? r.z + (z.lenB - r.w) : c;
-            ost = r.x == 0u ? z.stB : stt;
-        }
-        a.out_len[z.i] = olen;
-        a.status[z.i] = (uint8_t)ost;
-    }
-}
-
 // Long-literal phase of fill workgroup g = blockIdx.x (all kBlockAll threads call it, after the
 // fills; c1 / c2 = its class counts). kBlock threads decode (one wave queue of kQ entries each in
 // s_q), kU steps between refill points, kRing input dwords per lane in s_ring and a kOS-byte
@@ -266,8 +87,7 @@ __device__ __forceinline__ void split_join(const DecodeArgs& a, uint32_t nsplit,
 template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll>
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
-                                           const uint32_t* s_lut, const uint16_t* s_lo, uint32_t nsplit, uint4* s_rec) {
-    static_assert(HPK_SPLIT_K * (20 * 4 + 16) <= kBlock * kRing * 4, "split join: staging and results in the input rings");
+                                           const uint32_t* s_lut, const uint16_t* s_lo) {
     constexpr uint32_t kChunk = 64;            // list entries per claim (one per lane)
     constexpr uint32_t kQ = 2 * kChunk;        // per-wave queue: < 64 left + one claim
     // Output buffer per lane: bytes [lb, ob) of the output (lb 16-byte aligned) at [0, ob - lb). A
@@ -388,14 +208,8 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             }
             lv = ob - o0;
             sv = st;
-            // a split literal's piece: its end (bits left, bytes, status) to the workgroup's record;
-            // the length and status stores go past their buffers (dropped)
-            const bool spl = (idx >> 31) != 0u;
-            ia = spl ? 0xFFFFFFF0u : idx * 4u;
-            ja = spl ? 0xFFFFFFF0u : idx;
-            if (spl)
-                reinterpret_cast<uint2*>(s_rec)[2u * ((idx & 0x3FFFFFFFu) % (uint32_t)HPK_SPLIT_K) + ((idx >> 30) & 1u)] =
-                    make_uint2(Eb - X, (ob - o0) | (st << 24));
+            ia = idx * 4u;
+            ja = idx;
             __builtin_amdgcn_raw_buffer_store_b32(lv, r_len, ia, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sv, r_st, ja, 0, 0);
             act = false;
@@ -448,22 +262,11 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             const bool ok = e < total;
             const uint32_t lpos = ok ? (e < c1 ? ba + e : bb - 1u - (e - c1)) : ba;
             const uint32_t i0 = a.long_list[lpos];  // (a load either way: see the note below)
-            const uint32_t e0 = ok ? i0 : 0u;
+            const uint32_t i = ok ? i0 : 0u;
             // straight-line loads (no branch around them): a load under a branch leaves the compiler
             // unsure whether its register is still pending, and it then waits for all memory
-            // operations (the refill loads included) before the steps reuse the register.
-            // A split literal's piece (bit 31; bit 30: the second) is the literal's first half of
-            // input bytes, its output at the region's start, or the second half, its output at the
-            // region's end minus that half's decoded bound (the two never overlap: the first half
-            // decodes to at most its own bound); the entry keeps the flags for the finish.
-            const bool sp = (e0 >> 31) != 0u;
-            const uint32_t pi = a.split_pool[sp ? (e0 & 0x3FFFFFFFu) : 0u];
-            const uint32_t i = sp ? pi : e0;
-            const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], r0 = a.out_off[i], r1 = a.out_off[i + 1];
-            const uint32_t sm = p0 + ((p1 - p0) >> 1);
-            const bool second = sp && ((e0 >> 30) & 1u);
-            const uint4 li = make_uint4(e0, second ? sm : p0, sp && !second ? sm : p1,
-                                        second ? r1 - ((p1 - sm) * 8u) / 5u : r0);
+            // operations (the refill loads included) before the steps reuse the register
+            const uint4 li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.out_off[i]);
             const uint64_t lm = __ballot(ok);
             const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
             if (ok) sq[wv][(qt + lr) % kQ] = li;
@@ -587,7 +390,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
         pin(ia);
         pin(ja);
     }
-    if (nsplit) split_join<kBlock>(a, nsplit, s_rec, s_lo, r_out, in_end, s_ring);
     if (kDiag) {
         dg[0] = __builtin_amdgcn_s_memtime() - dt0;
         const uint32_t gw = blockIdx.x * (uint32_t)(kBlock / 64) + wv;
