@@ -28,6 +28,12 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_STAGGER
+#define HPK_STAGGER 1
+#endif
+#ifndef HPK_STAGGER_PH
+#define HPK_STAGGER_PH 2  // phases: workgroup b's first fill is (b % PH) / PH of a window
+#endif
 #ifndef HPK_LATE_FIN
 #define HPK_LATE_FIN 1  // 0: a finished lane literal's length and status are made in the finish round (v21)
 #endif
@@ -997,10 +1003,17 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     // (a greedy cut leaves a small last fill that still costs a whole fill's setup, slowest literal
     // and write-back); the effective window is that size plus a margin for literal granularity
     uint32_t kWe = (uint32_t)kW;
+    uint32_t kW0 = kWe;  // the first fill's window
     if (kEven) {
         const uint32_t R = r_end - min((min(a.in_off[BA], a.in_cap) + a.in_mis) & ~15u, r_end);
         const uint32_t nf = (R + (uint32_t)kW - 1u) / (uint32_t)kW;
         if (nf > 1u) kWe = min((uint32_t)kW, (R + nf - 1u) / nf + 512u);
+        // HPK_STAGGER: in a range of many fills, workgroup b's first fill is (b % PH) / PH of a window
+        // (a whole one for b % PH = 0), so the workgroups' write-back and prefetch bursts (~35 MB over
+        // the chip at once when all fills run in step) alternate instead of coinciding (config 5
+        // +0.7 % with PH = 2, +0.4 % with 4; a range of a few fills would pay a whole extra fill)
+        const uint32_t ph = blockIdx.x % (uint32_t)HPK_STAGGER_PH;
+        if (HPK_STAGGER && nf >= 8u && ph) kW0 = kWe * ph / (uint32_t)HPK_STAGGER_PH;
     }
 
     // write back one decoded fill from the LDS image: the output span [G0, G1) with 16-byte
@@ -1134,6 +1147,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     bool dense_tried = false;  // block-uniform (kLongK): the range's first fill was checked
     while (cur < BB) {  // block-uniform
         const uint32_t cntl = min((uint32_t)kQ, BB - cur);
+        const uint32_t kWf = cur == BA ? kW0 : kWe;
         const uint32_t base16 = gin & ~15u;
         const uint32_t ob16 = gout & ~15u;
         unsigned long long tb0 = 0;
@@ -1171,7 +1185,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             const uint32_t p0 = P.io0[r] + a.in_mis, p1 = P.io1[r] + a.in_mis;
             const uint32_t o0 = P.oo0[r] + a.out_mis, o1 = P.oo1[r] + a.out_mis;
             // fitting literals form a prefix (offsets are non-decreasing)
-            const bool fits = !bad && t < cntl && p1 - base16 <= kWe && o1 - ob16 <= (uint32_t)kImg;
+            const bool fits = !bad && t < cntl && p1 - base16 <= kWf && o1 - ob16 <= (uint32_t)kImg;
             pos[r] = 0xFFFFFFFFu;
             if (fits) {
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
