@@ -28,6 +28,9 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_PF_LOOP
+#define HPK_PF_LOOP 1
+#endif
 #ifndef HPK_STAGGER
 #define HPK_STAGGER 1
 #endif
@@ -949,17 +952,21 @@ template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChun
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
+    constexpr int kPfN = R + 1;  // load groups of one fill prefetch (a round of offsets each, the window chunks)
     constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : (kPredSt ? kPred : kDword));
     // v21: body steps without fit tests, the literals' last bits in a checked tail pass (lit12_fast)
     constexpr bool kFast = HPK_FAST && kStore == kPred && !kAcc && kLook == 2 && !HPK_RELOAD && !kDefer;
     // v22: lengths and statuses of the lane literals made after the lane loop (HPK_LATE_FIN)
     constexpr bool kLate = HPK_LATE_FIN && !kFast && kStore == kPred && !kAcc && !HPK_RELOAD && !kDefer && !kSpread;
+    // the next fill's prefetch issued from the lane loop, a load per round (HPK_PF_LOOP)
+    constexpr bool kPfLoop = HPK_PF_LOOP && kLate;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
     constexpr int kImg = kStore == kPred ? kO - 256 : kO;
     const uint32_t dmy = (uint32_t)kImg + (threadIdx.x & 63u) * 4u;
     static_assert(kChunk >= 64, "a refill can hand out 64 slots");
     unsigned long long t_start = 0, t_dec = 0, n_steps = 0, n_fills = 0, t_pre = 0, t_setA = 0, t_setB = 0, t_long = 0,
-                       t_A0 = 0, t_B0 = 0, t_tail = 0, t_byte = 0, t_rounds = 0, n_longs = 0;
+                       t_A0 = 0, t_B0 = 0, t_tail = 0, t_byte = 0, t_rounds = 0, n_longs = 0, t_sb1 = 0, t_sb2 = 0,
+                       t_sb3 = 0;
     if (kMode == 3) t_start = __builtin_amdgcn_s_memtime();
     __shared__ __attribute__((aligned(16))) uint8_t smem[G::kLdsBytes];
     uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
@@ -1332,6 +1339,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
         lds_barrier();
+        if (kMode == 3) t_sb1 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: scan, window in LDS)
         // queue entries: the fill's literals less those left to hpk_decode_long (kLongK)
         const uint32_t kq = kLongK ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(s_bbase[63] + s_hist[63])) : k;
 #pragma unroll
@@ -1347,10 +1355,43 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         // the next fill's offsets and window: in flight during this fill's decode. Unconditional
         // (clamped past the range end), so no register phi forces a wait on the stores below.
         const uint32_t cur_next = cur + k;
-        {
-            const uint32_t c = min(cur_next, BB - 1);
-            prefetch_fill<G::kBlock>(P, a, tid, c, min(c + (uint32_t)kQ, BB), gin_next & ~15u, rlast16);
+        // (block-uniform: held in scalar registers through the lane loop)
+        const uint32_t pf_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)min(cur_next, BB - 1));
+        const uint32_t pf_end = min(pf_c + (uint32_t)kQ, BB);
+        const uint32_t pf_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)(gin_next & ~15u));
+        // kPfLoop: the next fill's loads are issued one per lane-loop round (the first kPfN rounds)
+        // instead of all at once here, where every wave's loads and the write-back's stores queued
+        // at the CU's memory path together; what the loop does not issue goes out after it
+        uint32_t pf_i = 0;  // (wave-uniform) next load of the prefetch to issue
+        auto pf_part = [&](uint32_t j) {
+            // (addresses from an opaque copy of the round, so they are not hoisted out of the lane
+            // loop into registers it does not have)
+            uint32_t base = pf_c;
+            asm volatile("" : "+s"(base));
+            const uint32_t cntl = pf_end - base;
+#pragma unroll
+            for (int q = 0; q < kPfN; ++q) {
+                if (j == (uint32_t)q) {
+                    if (q < R) {  // round q of the offsets
+                        const uint32_t t = min(tid + (uint32_t)G::kBlock * q, cntl - 1);
+                        P.io0[q] = a.in_off[base + t];
+                        P.io1[q] = a.in_off[base + t + 1];
+                        P.oo0[q] = a.out_off[base + t];
+                        P.oo1[q] = a.out_off[base + t + 1];
+                    } else {  // the window chunks
+#pragma unroll
+                        for (int r = 0; r < S; ++r)
+                            P.chunk[r] = reinterpret_cast<const uint4*>(
+                                a.in_base)[min((pf_base >> 4) + (base - pf_c) + tid + (uint32_t)G::kBlock * r, rlast16)];
+                    }
+                }
+            }
+        };
+        if (!kPfLoop) {
+            prefetch_fill<G::kBlock>(P, a, tid, pf_c, pf_end, pf_base, rlast16);
+            pf_i = kPfN;
         }
+        if (kMode == 3) t_sb2 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: + queue, prefetch issued)
         // the previous fill's write-back: its image is read out before this fill decodes over it
         if (pk) {
             if (kDefer)
@@ -1362,6 +1403,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         pcur = cur;
         pG0 = gout;
         pG1 = gout_next;
+        if (kMode == 3) t_sb3 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: + write-back issued)
         lds_barrier();
         unsigned long long td0 = 0;
         if (kMode == 3) {
@@ -1547,6 +1589,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     #pragma unroll
                         for (int s = 0; s < kRefillN; ++s) lit12_step<kStore, kLook, kAcc>(L, win32, s_lut, s_lo, s_out, dmy);
                         if (kMode == 3) n_steps += kRefillN;
+                        if (kPfLoop && pf_i < (uint32_t)kPfN) pf_part(pf_i++);
                         const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
                         if (__any(fin)) {
                             const bool sw = fin & nv;
@@ -1612,6 +1655,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         if (kDefer)
             while (fs <= F) flush_slot(fs++);  // what the decode loops did not issue
+        while (pf_i < (uint32_t)kPfN) pf_part(pf_i++);  // (kPfLoop) the prefetch loads the loop did not issue
         unsigned long long tq0 = 0;
         if (kMode == 3) {
             tq0 = __builtin_amdgcn_s_memtime();
@@ -1655,8 +1699,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         a.dbg[gwi * 16 + 9] = t_B0;
         a.dbg[gwi * 16 + 10] = t_byte;
         a.dbg[gwi * 16 + 11] = t_end - t_tail;
-        a.dbg[gwi * 16 + 12] = t_rounds;
-        a.dbg[gwi * 16 + 13] = n_longs;
+        a.dbg[gwi * 16 + 12] = kCoop ? t_rounds : t_sb1;
+        a.dbg[gwi * 16 + 13] = kCoop ? n_longs : t_sb2;
+        a.dbg[gwi * 16 + 14] = t_sb3;
     }
     if (kLongK) {  // the literals this workgroup left to the long-literal phase
         lds_barrier();

@@ -56,7 +56,7 @@ if mode == 3:
     got = L.hpk_debug_stamps(buf.ctypes.data, buf.size)
     st8 = buf[:got].reshape(-1, 16).astype(np.int64)
     names = ["total", "decode", "steps", "barrier_wait", "pre", "setupA", "setupB", "long", "setupA_fill0",
-             "setupB_fill0", "byte_pass", "last_flush"]
+             "setupB_fill0", "byte_pass", "last_flush", "setupB_to_window", "setupB_to_prefetch", "setupB_to_flush"]
     res["stamps_per_wave"] = {nm: {"mean": round(float(st8[:, i].mean()), 1), "max": int(st8[:, i].max())}
                               for i, nm in enumerate(names)}
 if mode == 5:  # hpk_decode_long's per-wave counters
