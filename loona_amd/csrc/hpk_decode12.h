@@ -28,6 +28,9 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_FLUSH_TOP
+#define HPK_FLUSH_TOP 0  // 1: the previous fill's write-back at the top of a fill (config 5 687 vs 689 GiB/s: no gain)
+#endif
 #ifndef HPK_PF_LOOP
 #define HPK_PF_LOOP 1
 #endif
@@ -960,6 +963,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     constexpr bool kLate = HPK_LATE_FIN && !kFast && kStore == kPred && !kAcc && !HPK_RELOAD && !kDefer && !kSpread;
     // the next fill's prefetch issued from the lane loop, a load per round (HPK_PF_LOOP)
     constexpr bool kPfLoop = HPK_PF_LOOP && kLate;
+    // the previous fill's write-back issued at the top of a fill, before its setup (HPK_FLUSH_TOP)
+    constexpr bool kFlushTop = HPK_FLUSH_TOP && !kDefer;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
     constexpr int kImg = kStore == kPred ? kO - 256 : kO;
     const uint32_t dmy = (uint32_t)kImg + (threadIdx.x & 63u) * 4u;
@@ -1164,6 +1169,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             n_fills += t1 - tb0;  // (mode 3: barrier wait)
             tb0 = t1;
+        }
+        if (kFlushTop && pk) {  // the previous fill's write-back first: its stores drain under this setup
+            flush(pcur, pk, pG0, pG1);
+            pk = 0;
         }
         if (tid < 64) s_hist[tid] = 0;
         if (tid == 0) {
@@ -1393,7 +1402,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         if (kMode == 3) t_sb2 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: + queue, prefetch issued)
         // the previous fill's write-back: its image is read out before this fill decodes over it
-        if (pk) {
+        if (!kFlushTop && pk) {
             if (kDefer)
                 flush_read(pcur, pk, pG0, pG1);
             else
