@@ -28,6 +28,9 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_FLUSH_LOOP
+#define HPK_FLUSH_LOOP 0  // write-back rounds (<= 3) stored from the lane loop instead of before it (needs HPK_PF_LOOP)
+#endif
 #ifndef HPK_FLUSH_TOP
 #define HPK_FLUSH_TOP 0  // 1: the previous fill's write-back at the top of a fill (config 5 687 vs 689 GiB/s: no gain)
 #endif
@@ -955,7 +958,6 @@ template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, int kChun
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
-    constexpr int kPfN = R + 1;  // load groups of one fill prefetch (a round of offsets each, the window chunks)
     constexpr int kStore = kMode == 2 ? kNoStore : (kMode == 4 ? kChecked : (kPredSt ? kPred : kDword));
     // v21: body steps without fit tests, the literals' last bits in a checked tail pass (lit12_fast)
     constexpr bool kFast = HPK_FAST && kStore == kPred && !kAcc && kLook == 2 && !HPK_RELOAD && !kDefer;
@@ -963,6 +965,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     constexpr bool kLate = HPK_LATE_FIN && !kFast && kStore == kPred && !kAcc && !HPK_RELOAD && !kDefer && !kSpread;
     // the next fill's prefetch issued from the lane loop, a load per round (HPK_PF_LOOP)
     constexpr bool kPfLoop = HPK_PF_LOOP && kLate;
+    // HPK_FLUSH_LOOP: the previous fill's last S write-back rounds are read into the window-prefetch
+    // registers (free once the window is in LDS) and stored from the lane loop, before the window's
+    // prefetch loads reuse those registers
+    constexpr int kFD = kPfLoop ? (HPK_FLUSH_LOOP < S ? HPK_FLUSH_LOOP : S) : 0;
+    // groups of one fill prefetch: a round of offsets each, the deferred write-back rounds, the window
+    constexpr int kPfN = R + kFD + 1;
     // the previous fill's write-back issued at the top of a fill, before its setup (HPK_FLUSH_TOP)
     constexpr bool kFlushTop = HPK_FLUSH_TOP && !kDefer;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
@@ -1130,6 +1138,46 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
     };
     uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
+    uint32_t fd_c0 = 0, fd_mask = 0;  // kFD: first image chunk of the deferred rounds' fill, rounds holding data
+    Prefetch<R, S> P;
+    // kFD: the write-back with its last kFD rounds read into P.chunk (stored by pf_part)
+    auto flush_split = [&](uint32_t fcur, uint32_t fk, uint32_t G0, uint32_t G1) {
+        const uint32_t ob = G0 & ~15u;
+        const uint32_t c0 = ob >> 4, c1 = (G1 + 15) >> 4;
+        const uint4* l16 = reinterpret_cast<const uint4*>(s_out);
+        uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
+        fd_c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c0);
+        fd_mask = 0;
+#pragma unroll
+        for (int r = 0; r < G::kFlushRounds; ++r) {
+            const uint32_t ci = c0 + tid + (uint32_t)G::kBlock * r;
+            const bool ok = ci < c1 && (ci << 4) >= G0 && (ci << 4) + 16u <= G1;
+            if (r < G::kFlushRounds - kFD) {
+                if (ok) g16[ci] = l16[ci - c0];
+            } else if (kFD) {
+                const int d = r - (G::kFlushRounds - kFD);
+                if (ok) {
+                    P.chunk[d < S ? d : 0] = l16[ci - c0];
+                    fd_mask |= 1u << d;
+                }
+            }
+        }
+        if (tid < 32) {  // the partial chunks at the two ends, one byte per lane
+            const uint32_t g = tid < 16 ? c0 << 4 : (c1 - 1) << 4;
+            const bool partial = !(g >= G0 && g + 16u <= G1) && (tid < 16 || c1 - 1 != c0);
+            const uint32_t x = g + (tid & 15u);
+            if (partial && x >= G0 && x < G1) a.out_base[x] = s_out[x - ob];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = tid + (uint32_t)G::kBlock * r;
+            if (i < fk) {
+                const uint32_t v = s_lenst[i];
+                a.out_len[fcur + i] = v & 0xFFFFFFu;
+                a.status[fcur + i] = (uint8_t)(v >> 24);
+            }
+        }
+    };
     // kLongK: long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
     auto leave = [&](uint32_t i, uint32_t nb) {
@@ -1149,7 +1197,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
 
     uint32_t cur = BA;
     uint32_t gin = 0, gout = 0;  // exact input / output start of the fill (blob-relative + mis)
-    Prefetch<R, S> P;
     if (cur < BB) {
         gin = a.in_off[cur] + a.in_mis;
         gout = a.out_off[cur] + a.out_mis;
@@ -1387,6 +1434,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                         P.io1[q] = a.in_off[base + t + 1];
                         P.oo0[q] = a.out_off[base + t];
                         P.oo1[q] = a.out_off[base + t + 1];
+                    } else if (q < R + kFD) {  // a deferred write-back round (stored before the window's loads)
+                        const int d = q - R;
+                        if ((fd_mask >> d) & 1u)
+                            reinterpret_cast<uint4*>(a.out_base)[fd_c0 + (base - pf_c) + tid +
+                                                                 (uint32_t)G::kBlock * (G::kFlushRounds - kFD + d)] =
+                                P.chunk[d < S ? d : 0];
                     } else {  // the window chunks
 #pragma unroll
                         for (int r = 0; r < S; ++r)
@@ -1402,9 +1455,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         if (kMode == 3) t_sb2 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: + queue, prefetch issued)
         // the previous fill's write-back: its image is read out before this fill decodes over it
+        fd_mask = 0;
         if (!kFlushTop && pk) {
             if (kDefer)
                 flush_read(pcur, pk, pG0, pG1);
+            else if (kFD)
+                flush_split(pcur, pk, pG0, pG1);
             else
                 flush(pcur, pk, pG0, pG1);
         }
