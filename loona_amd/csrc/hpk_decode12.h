@@ -29,7 +29,7 @@
 #include "hpk_split.h"
 
 #ifndef HPK_FLUSH_LOOP
-#define HPK_FLUSH_LOOP 0  // write-back rounds (<= 3) stored from the lane loop instead of before it (needs HPK_PF_LOOP)
+#define HPK_FLUSH_LOOP 1  // write-back rounds (<= 3) stored from the lane loop instead of before it (needs HPK_PF_LOOP; 1: config 5 +1 %, 2 spill)
 #endif
 #ifndef HPK_FLUSH_TOP
 #define HPK_FLUSH_TOP 0  // 1: the previous fill's write-back at the top of a fill (config 5 687 vs 689 GiB/s: no gain)
