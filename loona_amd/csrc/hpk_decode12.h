@@ -31,9 +31,6 @@
 #ifndef HPK_FLUSH_LOOP
 #define HPK_FLUSH_LOOP 1  // write-back rounds (<= 3) stored from the lane loop instead of before it (needs HPK_PF_LOOP; 1: config 5 +1 %, 2 spill)
 #endif
-#ifndef HPK_LENST_LOOP
-#define HPK_LENST_LOOP 0  // 1: the previous fill's lengths and statuses stored from the lane loop (needs HPK_FLUSH_LOOP)
-#endif
 #ifndef HPK_FLUSH_TOP
 #define HPK_FLUSH_TOP 0  // 1: the previous fill's write-back at the top of a fill (config 5 687 vs 689 GiB/s: no gain)
 #endif
@@ -972,12 +969,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     // registers (free once the window is in LDS) and stored from the lane loop, before the window's
     // prefetch loads reuse those registers
     constexpr int kFD = kPfLoop ? (HPK_FLUSH_LOOP < S ? HPK_FLUSH_LOOP : S) : 0;
-    // HPK_LENST_LOOP: the previous fill's lengths and statuses stored from the lane loop too (s_lenst
-    // keeps them until the lane literals' lengths are made after the loop)
-    constexpr int kLD = (HPK_LENST_LOOP && kFD && kCoop == 0 && kMode != 1) ? R : 0;
-    // groups of one fill prefetch: a round of offsets each, the deferred write-back rounds, the
-    // deferred length rounds, the window
-    constexpr int kPfN = R + kFD + kLD + 1;
+    // groups of one fill prefetch: a round of offsets each, the deferred write-back rounds, the window
+    constexpr int kPfN = R + kFD + 1;
     // the previous fill's write-back issued at the top of a fill, before its setup (HPK_FLUSH_TOP)
     constexpr bool kFlushTop = HPK_FLUSH_TOP && !kDefer;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
@@ -1146,7 +1139,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     };
     uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;  // the previous fill, not yet written back
     uint32_t fd_c0 = 0, fd_mask = 0;  // kFD: first image chunk of the deferred rounds' fill, rounds holding data
-    uint32_t fd_cur = 0, fd_k = 0;    // kLD: the deferred lengths' fill (first literal, count; 0: none)
     Prefetch<R, S> P;
     // kFD: the write-back with its last kFD rounds read into P.chunk (stored by pf_part)
     auto flush_split = [&](uint32_t fcur, uint32_t fk, uint32_t G0, uint32_t G1) {
@@ -1176,10 +1168,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             const uint32_t x = g + (tid & 15u);
             if (partial && x >= G0 && x < G1) a.out_base[x] = s_out[x - ob];
         }
-        fd_cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)fcur);
-        fd_k = kLD ? (uint32_t)__builtin_amdgcn_readfirstlane((int)fk) : 0u;
 #pragma unroll
-        for (int r = 0; r < R && !kLD; ++r) {
+        for (int r = 0; r < R; ++r) {
             const uint32_t i = tid + (uint32_t)G::kBlock * r;
             if (i < fk) {
                 const uint32_t v = s_lenst[i];
@@ -1444,13 +1434,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                         P.io1[q] = a.in_off[base + t + 1];
                         P.oo0[q] = a.out_off[base + t];
                         P.oo1[q] = a.out_off[base + t + 1];
-                    } else if (q >= R + kFD && q < R + kFD + kLD) {  // a round of the deferred lengths, statuses
-                        const uint32_t i = tid + (uint32_t)G::kBlock * (q - R - kFD) + (base - pf_c);
-                        if (i < fd_k) {
-                            const uint32_t v = s_lenst[i];
-                            a.out_len[fd_cur + i] = v & 0xFFFFFFu;
-                            a.status[fd_cur + i] = (uint8_t)(v >> 24);
-                        }
                     } else if (q < R + kFD) {  // a deferred write-back round (stored before the window's loads)
                         const int d = q - R;
                         if ((fd_mask >> d) & 1u)
@@ -1473,7 +1456,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         if (kMode == 3) t_sb2 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: + queue, prefetch issued)
         // the previous fill's write-back: its image is read out before this fill decodes over it
         fd_mask = 0;
-        fd_k = 0;
         if (!kFlushTop && pk) {
             if (kDefer)
                 flush_read(pcur, pk, pG0, pG1);
@@ -1687,9 +1669,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                             if (!__any(!fin | sw)) break;
                         }
                     }
-                    // the prefetch groups the loop did not issue, before the lengths below overwrite the
-                    // previous fill's (kLD)
-                    while (kPfLoop && pf_i < (uint32_t)kPfN) pf_part(pf_i++);
                     if (s1) {
                         const uint2 e = lq[t1];
                         const uint32_t Eb = (e.x & 0xFFFFu) * 8u + 31u + (e.x >> 16) * 8u;
