@@ -28,6 +28,9 @@
 #include "hpk_decode_kernel.h"
 #include "hpk_split.h"
 
+#ifndef HPK_FD_FIRST
+#define HPK_FD_FIRST 0  // 1: the write-back rounds deferred to the lane loop are the first (always full), not the last
+#endif
 #ifndef HPK_FLUSH_LOOP
 #define HPK_FLUSH_LOOP 1  // write-back rounds (<= 3) stored from the lane loop instead of before it (needs HPK_PF_LOOP; 1: config 5 +1 %, 2 spill)
 #endif
@@ -1152,10 +1155,10 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         for (int r = 0; r < G::kFlushRounds; ++r) {
             const uint32_t ci = c0 + tid + (uint32_t)G::kBlock * r;
             const bool ok = ci < c1 && (ci << 4) >= G0 && (ci << 4) + 16u <= G1;
-            if (r < G::kFlushRounds - kFD) {
+            if (HPK_FD_FIRST ? r >= kFD : r < G::kFlushRounds - kFD) {
                 if (ok) g16[ci] = l16[ci - c0];
             } else if (kFD) {
-                const int d = r - (G::kFlushRounds - kFD);
+                const int d = HPK_FD_FIRST ? r : r - (G::kFlushRounds - kFD);
                 if (ok) {
                     P.chunk[d < S ? d : 0] = l16[ci - c0];
                     fd_mask |= 1u << d;
@@ -1438,7 +1441,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                         const int d = q - R;
                         if ((fd_mask >> d) & 1u)
                             reinterpret_cast<uint4*>(a.out_base)[fd_c0 + (base - pf_c) + tid +
-                                                                 (uint32_t)G::kBlock * (G::kFlushRounds - kFD + d)] =
+                                                                 (uint32_t)G::kBlock * (HPK_FD_FIRST ? d : G::kFlushRounds - kFD + d)] =
                                 P.chunk[d < S ? d : 0];
                     } else {  // the window chunks
 #pragma unroll
