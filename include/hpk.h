@@ -126,7 +126,11 @@ int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
                      uint8_t* status, int flags);
 
 /* Read and clear the context's sticky device error flag (after HPK_ASYNC calls; synchronises the
- * ctx stream). Returns HPK_E_OK, HPK_E_INVAL (some call saw bad offsets) or HPK_E_DEVICE. */
+ * ctx stream). Returns HPK_E_OK, HPK_E_INVAL (some call saw bad offsets) or HPK_E_DEVICE.
+ * The flag belongs to the context, not to a stream: it reports a bad call made on any stream the
+ * context was bound to (hpk_ctx_set_stream) once that call has run, so after async calls on
+ * several streams synchronise each of them before relying on the answer; a synchronous call
+ * returns (and clears) a flag left by an earlier async call on another stream. */
 int hpk_ctx_check(hpk_ctx* ctx);
 
 /* ---- batch calls on the host CPU ----------------------------------------
@@ -298,6 +302,11 @@ typedef struct hpk_henc_out {
 int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const uint8_t* fields, const uint32_t* field_off,
                            const uint32_t* hdr_off, uint32_t nblocks, hpk_henc_out* out);
 void hpk_henc_out_free(hpk_henc_out* out);
+/* A failed hpk_henc_encode_blocks (any negative return) leaves every encoder's dynamic table as it
+ * was before the call, as a failed hpk_henc_encode does; the blocks are then not sent at all.
+ * Testing only: the calling thread's next n Huffman batches inside hpk_henc_encode_blocks fail
+ * with HPK_E_DEVICE (n = 0 clears it), so that guarantee can be checked without a device fault. */
+void hpk_test_fail_batches(int n);
 
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);

@@ -78,6 +78,7 @@ EXPORTS = (
     "hpk_henc_encode",
     "hpk_henc_encode_blocks",
     "hpk_henc_out_free",
+    "hpk_test_fail_batches",
     "hpk_version",
 )
 
@@ -223,6 +224,8 @@ def lib() -> ctypes.CDLL:
         L.hpk_henc_encode_blocks.restype = ctypes.c_int
         L.hpk_henc_out_free.argtypes = [ctypes.POINTER(HencOut)]
         L.hpk_henc_out_free.restype = None
+        L.hpk_test_fail_batches.argtypes = [ctypes.c_int]
+        L.hpk_test_fail_batches.restype = None
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

@@ -74,22 +74,23 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     return c;
 }
 
-int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list) {
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
     int j = -1;
     for (int k = 0; k < hpk_ctx::kLongSlots; ++k)
         if (c->long_list[k] && c->long_stream[k] == c->stream) j = k;
     if (j < 0) {
         j = 0;
         while (j < hpk_ctx::kLongSlots && c->long_list[j]) ++j;
-        if (j == hpk_ctx::kLongSlots) {  // all taken: reuse the oldest once its stream has drained
+        if (j == hpk_ctx::kLongSlots) {  // all taken: reuse the oldest once its last launch is done
             j = c->long_next;
             c->long_next = (j + 1) % hpk_ctx::kLongSlots;
-            HIP_TRY(hipStreamSynchronize(c->long_stream[j]));
+            if (c->long_ev_set[j]) HIP_TRY(hipEventSynchronize(c->long_ev[j]));
         }
         c->long_stream[j] = c->stream;
     }
+    if (!c->long_ev[j]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[j], hipEventDisableTiming));
     if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->long_ev_set[j]) HIP_TRY(hipEventSynchronize(c->long_ev[j]));
         (void)hipFree(c->long_list[j]);
         c->long_list[j] = nullptr;
         c->long_list_cap[j] = 0;
@@ -98,6 +99,13 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list) {
         c->long_list_cap[j] = cap;
     }
     *list = c->long_list[j];
+    *slot = j;
+    return HPK_E_OK;
+}
+
+int hpk_long_list_used(hpk_ctx* c, int slot) {
+    HIP_TRY(hipEventRecord(c->long_ev[slot], c->stream));
+    c->long_ev_set[slot] = true;
     return HPK_E_OK;
 }
 
@@ -115,8 +123,11 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
-    for (int j = 0; j < hpk_ctx::kLongSlots; ++j)
+    for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
+        if (c->long_ev_set[j]) (void)hipEventSynchronize(c->long_ev[j]);
         if (c->long_list[j]) (void)hipFree(c->long_list[j]);
+        if (c->long_ev[j]) (void)hipEventDestroy(c->long_ev[j]);
+    }
     for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
         if (c->ev_in[j]) (void)hipEventDestroy(c->ev_in[j]);
         if (c->ev_run[j]) (void)hipEventDestroy(c->ev_run[j]);

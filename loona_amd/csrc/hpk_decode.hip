@@ -118,7 +118,8 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.out_cap = b.out_cap;
     a.err = c->d_err;
     uint32_t* ll = nullptr;
-    if (int rc = hpk_long_list(c, b.n, &ll)) return rc;
+    int lslot = 0;
+    if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
     a.long_list = ll;
     a.long_min = HPK_LONG_MIN;
     a.long_big = HPK_LONG_BIG;
@@ -176,6 +177,5 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
 #endif
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipGetLastError());
-    return HPK_E_OK;
+    return hpk_long_list_used(c, lslot);
 }

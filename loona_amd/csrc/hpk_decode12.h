@@ -1220,6 +1220,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             n_fills += t1 - tb0;  // (mode 3: barrier wait)
             tb0 = t1;
         }
+        // the long-list counts before this fill (nothing changes them until the setup below): a fill
+        // found bad takes back what its own literals listed
+        const uint32_t lcnt6 = kLongK ? s_ctr[6] : 0u, lcnt7 = kLongK ? s_ctr[7] : 0u;
         if (kFlushTop && pk) {  // the previous fill's write-back first: its stores drain under this setup
             flush(pcur, pk, pG0, pG1);
             pk = 0;
@@ -1305,7 +1308,13 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 a.out_len[i] = 0;
                 a.status[i] = (uint8_t)HPK_BAD_OFFSETS;
             }
-            if (tid == 0) *a.err = 1u;
+            if (tid == 0) {
+                *a.err = 1u;
+                if (kLongK) {  // this fill's long literals are void too: not for the long-literal phase
+                    s_ctr[6] = lcnt6;
+                    s_ctr[7] = lcnt7;
+                }
+            }
             break;
         }
         if (kLongK && !dense_tried) {

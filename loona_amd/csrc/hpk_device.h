@@ -38,17 +38,23 @@ struct hpk_ctx {
     uint32_t* h_err = nullptr;
     uint32_t* d_err = nullptr;
     // the long-literal list per stream (calls on different streams may overlap): one u32 per
-    // literal of the batch, grow-only
+    // literal of the batch, grow-only. A slot's event is recorded after the launch that used it; a
+    // slot taken over from another stream (or grown) is reused only once that event has completed,
+    // whatever became of the stream that recorded it.
     static constexpr int kLongSlots = 8;
     hipStream_t long_stream[kLongSlots] = {};
+    hipEvent_t long_ev[kLongSlots] = {};
+    bool long_ev_set[kLongSlots] = {};
     uint32_t* long_list[kLongSlots] = {};
     size_t long_list_cap[kLongSlots] = {};
     int long_next = 0;
 };
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on
-// first use; HPK_E_OK or an error code).
-int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list);
+// first use; HPK_E_OK or an error code); *slot is passed to hpk_long_list_used after the launch.
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot);
+// Records the slot's event on the context's stream after the launch that reads the list.
+int hpk_long_list_used(hpk_ctx* c, int slot);
 
 // One batch call as the launchers see it: capacities clamped to HPK_MAX_OFFSET (offsets above
 // them are bad whatever the buffer size).

@@ -137,12 +137,14 @@ extern "C" int hpk_h2_read_frames(hpk_ctx* ctx, hpk_h2conn* const* conns, const 
                 n -= pad;
             }
             if (k->pending) {  // read_headers' CONTINUATION loop (server.rs:1376-1417)
-                if (type != kContinuation) {
-                    err = HPK_H2_EXPECTED_CONTINUATION_FRAME;
-                    break;
-                }
+                // the stream id is checked before the frame type (server.rs:1391-1397, then 1399-1408):
+                // any frame of another stream is ExpectedContinuationForStream, whatever its type
                 if (sid != k->pend_stream) {
                     err = HPK_H2_EXPECTED_CONTINUATION_FOR_STREAM;
+                    break;
+                }
+                if (type != kContinuation) {
+                    err = HPK_H2_EXPECTED_CONTINUATION_FRAME;
                     break;
                 }
                 k->frag.insert(k->frag.end(), p, p + n);

@@ -19,11 +19,14 @@
 
 #include <chrono>
 #include <deque>
+#include <unordered_map>
 #include <thread>
 #include <string>
 #include <vector>
 
 #include "../../include/hpk.h"
+
+int hpk_set_err_msg(const char* what, int code);  // hpk_ctx.hip: hpk_last_error's message
 
 namespace {
 
@@ -733,6 +736,11 @@ extern "C" int hpk_henc_encode(hpk_henc* e, const uint8_t* fields, const uint32_
 // ONE batch (hpk_encode_batch through ctx, or the library's CPU batch path), and each block is
 // assembled with the H-bit form wherever it is strictly shorter — the same bytes as hpk_henc_encode
 // block by block.
+// Test hook (include/hpk.h): the next n Huffman batches made by hpk_henc_encode_blocks fail as a
+// device error would, so tests can check that a failed call leaves every encoder as it was.
+static thread_local int t_fail_batches = 0;
+extern "C" void hpk_test_fail_batches(int n) { t_fail_batches = n > 0 ? n : 0; }
+
 extern "C" int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const uint8_t* fields,
                                       const uint32_t* field_off, const uint32_t* hdr_off, uint32_t nblocks,
                                       hpk_henc_out* out) {
@@ -745,6 +753,21 @@ extern "C" int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const
     for (uint32_t k = 2 * hdr_off[0]; k < 2 * hdr_off[nblocks]; ++k)
         if (field_off[k + 1] < field_off[k]) return HPK_E_INVAL;
     if (nh && field_off[2 * hdr_off[nblocks]] > field_off[2 * hdr_off[0]] && !fields) return HPK_E_INVAL;
+    // Pass 1 runs against a working copy of each distinct encoder (hpk_henc_encode's `next = *e`);
+    // the copies replace the encoders only once every block is assembled, so a call that fails in
+    // the Huffman batch or the assembly leaves each dynamic table as it was and the peer's decoder
+    // never sees an index to an entry whose header was not sent.
+    std::unordered_map<hpk_henc*, size_t> slot;
+    std::vector<hpk_henc> work;
+    std::vector<size_t> wk(nblocks);
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        auto it = slot.find(encs[b]);
+        if (it == slot.end()) {
+            it = slot.emplace(encs[b], work.size()).first;
+            work.push_back(*encs[b]);
+        }
+        wk[b] = it->second;
+    }
     // pass 1: representation of every header; strings to code are recorded as (field start, length)
     struct Op {
         uint32_t raw_at, raw_len;  // bytes already final (prefix integers) in `raw`
@@ -756,7 +779,7 @@ extern "C" int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const
     std::vector<uint32_t> s_at, s_len;  // string k = fields[s_at[k] .. + s_len[k])
     std::vector<uint8_t> s_huff;        // its encoder Huffman-codes
     for (uint32_t b = 0; b < nblocks; ++b) {
-        hpk_henc& e = *encs[b];
+        hpk_henc& e = work[wk[b]];
         auto lit = [&](uint32_t at, uint32_t len) {
             ops.push_back(Op{(uint32_t)raw.size(), 0u, (uint32_t)s_at.size()});
             s_at.push_back(at);
@@ -788,36 +811,44 @@ extern "C" int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const
         }
         ops_off[b + 1] = (uint32_t)ops.size();
     }
-    // pass 2: one Huffman batch for the strings of Huffman-coding encoders
+    // pass 2: one Huffman batch for the strings of Huffman-coding encoders (u32 offsets: the strings
+    // and their encoded bounds must each fit below HPK_MAX_OFFSET)
     const uint32_t ns = (uint32_t)s_at.size();
     std::vector<uint32_t> bi(ns, UINT32_MAX);  // string -> batch index
     std::vector<uint32_t> in_off(1, 0), eo(1, 0);
     std::vector<uint8_t> in;
+    uint64_t eo_sum = 0;
     for (uint32_t k = 0; k < ns; ++k) {
         if (!s_huff[k]) continue;
         bi[k] = (uint32_t)in_off.size() - 1;
         in.insert(in.end(), fields + s_at[k], fields + s_at[k] + s_len[k]);
+        eo_sum += (hpk_encoded_bound(s_len[k]) + 3) & ~(uint64_t)3;
+        if (in.size() > HPK_MAX_OFFSET || eo_sum > HPK_MAX_OFFSET)
+            return hpk_set_err_msg("Huffman strings of one call exceed the u32 offset range", HPK_E_INVAL);
         in_off.push_back((uint32_t)in.size());
-        eo.push_back(eo.back() + (uint32_t)((hpk_encoded_bound(s_len[k]) + 3) & ~(size_t)3));
+        eo.push_back((uint32_t)eo_sum);
     }
     const uint32_t nb = (uint32_t)in_off.size() - 1;
     std::vector<uint8_t> enc(eo.back() ? eo.back() : 1), est(nb ? nb : 1);
     std::vector<uint32_t> elen(nb ? nb : 1);
     if (nb) {
         if (in.empty()) in.push_back(0);
-        const int rc = ctx ? hpk_encode_batch(ctx, in.data(), in.size(), in_off.data(), nb, enc.data(), enc.size(),
-                                              eo.data(), elen.data(), est.data(), HPK_PTR_HOST)
-                           : hpk_encode_batch_cpu(in.data(), in_off.data(), nb, enc.data(), eo.data(), elen.data(),
-                                                  est.data(), 0);
+        int rc;
+        if (t_fail_batches > 0) {
+            --t_fail_batches;
+            rc = hpk_set_err_msg("injected batch failure (hpk_test_fail_batches)", HPK_E_DEVICE);
+        } else {
+            rc = ctx ? hpk_encode_batch(ctx, in.data(), in.size(), in_off.data(), nb, enc.data(), enc.size(), eo.data(),
+                                        elen.data(), est.data(), HPK_PTR_HOST)
+                     : hpk_encode_batch_cpu(in.data(), in_off.data(), nb, enc.data(), eo.data(), elen.data(), est.data(),
+                                            0);
+        }
         if (rc) return rc;
     }
     // pass 3: assemble every block
     std::vector<uint8_t> o;
     o.reserve(raw.size() + in.size() + 16);
-    out->n_blocks = nblocks;
-    out->block_off = (uint32_t*)malloc((nblocks + 1) * sizeof(uint32_t));
-    if (!out->block_off) return HPK_E_INVAL;
-    out->block_off[0] = 0;
+    std::vector<uint32_t> boff(nblocks + 1, 0);
     for (uint32_t b = 0; b < nblocks; ++b) {
         for (uint32_t q = ops_off[b]; q < ops_off[b + 1]; ++q) {
             const Op& op = ops[q];
@@ -835,16 +866,21 @@ extern "C" int hpk_henc_encode_blocks(hpk_ctx* ctx, hpk_henc* const* encs, const
                 o.insert(o.end(), fields + s_at[k], fields + s_at[k] + n);
             }
         }
-        if (o.size() >= (1ull << 32)) return HPK_E_INVAL;
-        out->block_off[b + 1] = (uint32_t)o.size();
+        if (o.size() >= (1ull << 32)) return hpk_set_err_msg("encoded blocks exceed 4 GiB", HPK_E_INVAL);
+        boff[b + 1] = (uint32_t)o.size();
     }
-    out->len = o.size();
+    out->block_off = (uint32_t*)malloc((nblocks + 1) * sizeof(uint32_t));
     out->bytes = (uint8_t*)malloc(o.size() ? o.size() : 1);
-    if (!out->bytes) {
+    if (!out->block_off || !out->bytes) {
         hpk_henc_out_free(out);
         return HPK_E_INVAL;
     }
+    memcpy(out->block_off, boff.data(), (nblocks + 1) * sizeof(uint32_t));
     if (!o.empty()) memcpy(out->bytes, o.data(), o.size());
+    out->n_blocks = nblocks;
+    out->len = o.size();
+    // commit: every encoder takes its working copy's table
+    for (const auto& kv : slot) *kv.first = std::move(work[kv.second]);
     return HPK_E_OK;
 }
 

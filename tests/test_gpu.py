@@ -598,6 +598,42 @@ def test_bad_device_offsets(codec, kind):
     assert (g[:guard] == 0xAB).all() and (g[-guard:] == 0xAB).all()
 
 
+def test_bad_offsets_with_long_literals_in_the_fill(codec):
+    """A bad literal's fill also holds long literals (>= 64 encoded bytes, left to the long-literal
+    phase): the whole rest of the workgroup's range gets HPK_BAD_OFFSETS with out_len 0, and the
+    long-literal phase must not decode those long literals afterwards (hpk.h contract); long
+    literals of valid ranges elsewhere still decode."""
+    from loona_amd import _lib, huffman_encode
+    from loona_amd.batch import decode_offsets_np
+
+    rng = np.random.default_rng(3)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;,/: ", np.uint8)
+    j = 12345
+    lits = []
+    for i in range(20000):
+        long_ = (j < i <= j + 6) or i % 997 == 0
+        n = int(rng.integers(120, 600)) if long_ else int(rng.integers(4, 50))
+        lits.append(huffman_encode(rng.choice(alpha, n).tobytes()))
+    blob, off = pack(lits)
+    n = len(lits)
+    io = np.asarray(off, np.int64).copy()
+    oo = decode_offsets_np(np.asarray(off, np.uint32)).astype(np.int64)
+    io[j] = io[j + 1] + 3  # decreasing: literal j is bad
+    out = torch.full((int(oo[-1]) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    ol = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    with pytest.raises(RuntimeError, match="hpk_decode_batch"):
+        codec.decode_into(to_dev(blob), to_dev(io.astype(np.uint32).view(np.int32)), out,
+                          to_dev(oo.astype(np.uint32).view(np.int32)), ol, st, device=True, sync=True)
+    stn, oln = st.cpu().numpy(), ol.cpu().numpy()
+    bad = stn == _lib.HPK_BAD_OFFSETS
+    assert bad[j : j + 7].all(), stn[j : j + 7]  # the long literals after j in its fill included
+    assert (oln[bad] == 0).all()
+    assert set(np.unique(stn)) <= {0, _lib.HPK_BAD_OFFSETS}
+    good_long = [i for i in range(0, n, 997) if not bad[i]]
+    assert len(good_long) > 10 and all(stn[i] == 0 and oln[i] > 0 for i in good_long)
+
+
 def _prefix_host(out, oo, ol, st, k):
     """The first k literals of a device decode as numpy (out_blob, out_off, out_len, status)."""
     end = int(oo[k].item()) & 0xFFFFFFFF
@@ -679,19 +715,37 @@ def test_h2_frames_replay_on_device(codec):
 
 def test_encode_blocks_on_device(codec):
     """SURVEY §8f-2 through the device: many responses' header blocks with every Huffman string in
-    one device encode batch == the CPU batch path == hpk_henc_encode block by block."""
+    one device encode batch, compared block by block with the encoder.rs restatement
+    (oracle/hpack_ref.Encoder(huffman=True): Encoder::encode, encoder.rs:210-234, with the H bit set
+    where the Huffman form is strictly shorter than encode_string_literal's raw form,
+    encoder.rs:296-307) on the same lists (interop headers plus random binary and numeric values),
+    and with hpk_henc_encode block by block. A failed device call leaves the encoders unchanged."""
     from test_hpack_encoder import response_lists
 
-    from loona_amd import hpack
+    from hpk_util import hpack_ref
+    from loona_amd import _lib, hpack
 
     lists = response_lists(seed=5)
     k = 5
     assert hpack.encode_blocks([], codec) == []
     encs_d = [hpack.Encoder(huffman=True) for _ in range(k)]
     encs_s = [hpack.Encoder(huffman=True) for _ in range(k)]
+    refs = [hpack_ref.Encoder(huffman=True) for _ in range(k)]
     got = hpack.encode_blocks([(encs_d[i % k], hs) for i, hs in enumerate(lists)], codec)
-    want = [encs_s[i % k].encode(hs) for i, hs in enumerate(lists)]
-    assert got == want
+    oracle = [refs[i % k].encode(hs) for i, hs in enumerate(lists)]
+    assert got == oracle
+    assert got == [encs_s[i % k].encode(hs) for i, hs in enumerate(lists)]
+    # a call failing after the table pass commits nothing: the next one matches the oracle again
+    more = response_lists(seed=6, n=200)
+    L = _lib.lib()
+    L.hpk_test_fail_batches(1)
+    try:
+        with pytest.raises(RuntimeError, match="injected"):
+            hpack.encode_blocks([(encs_d[i % k], hs) for i, hs in enumerate(more)], codec)
+    finally:
+        L.hpk_test_fail_batches(0)
+    got = hpack.encode_blocks([(encs_d[i % k], hs) for i, hs in enumerate(more)], codec)
+    assert got == [refs[i % k].encode(hs) for i, hs in enumerate(more)]
 
 
 def test_scatter_decode_gather_device_world1(codec):

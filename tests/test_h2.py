@@ -138,9 +138,25 @@ def test_httpwg_priority_frame_while_sending_headers():
 
 def test_httpwg_headers_frame_to_another_stream():
     """_4_http_frames.rs:215-250: HEADERS without END_HEADERS, then HEADERS for another stream ->
-    ExpectedContinuationFrame (server.rs:1399-1408), PROTOCOL_ERROR."""
+    ExpectedContinuationForStream, PROTOCOL_ERROR. read_headers compares the stream id before the
+    frame type (server.rs:1391-1397, then 1399-1408), so the other stream wins over the wrong type."""
     r, _ = one([h2.frame(HEADERS, 0, 1, BLOCK), h2.frame(HEADERS, END_HEADERS, 3, BLOCK)])
-    assert r.errors == ["ExpectedContinuationFrame"] and h2.error_code(r.errors[0]) == "PROTOCOL_ERROR"
+    assert r.errors == ["ExpectedContinuationForStream"] and h2.error_code(r.errors[0]) == "PROTOCOL_ERROR"
+    assert r.blocks == []
+
+
+@pytest.mark.parametrize("second,err", [
+    # same stream, wrong type: only the type check fails (server.rs:1399-1408)
+    (h2.frame(DATA, 0, 1, b"xyz"), "ExpectedContinuationFrame"),
+    (h2.frame(HEADERS, END_HEADERS, 1, BLOCK), "ExpectedContinuationFrame"),
+    # another stream, any type: the stream check comes first (server.rs:1391-1397)
+    (h2.frame(DATA, 0, 3, b"xyz"), "ExpectedContinuationForStream"),
+    (h2.frame(CONTINUATION, END_HEADERS, 3, BLOCK[5:]), "ExpectedContinuationForStream"),
+    (h2.frame(PING, 0, 0, b"12345678"), "ExpectedContinuationForStream"),
+])
+def test_continuation_check_order(second, err):
+    r, c = one([h2.frame(HEADERS, 0, 1, BLOCK[:5]), second])
+    assert r.errors == [err] and h2.error_code(err) == "PROTOCOL_ERROR" and c.error == err
     assert r.blocks == []
 
 

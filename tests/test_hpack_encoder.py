@@ -165,3 +165,44 @@ def test_encode_blocks_matches_block_by_block(huffman):
     decs = [hpack.Decoder() for _ in range(k)]
     back = hpack.decode_blocks([(decs[i % k], b) for i, b in enumerate(got)], None)
     assert back == lists
+
+
+@pytest.mark.parametrize("huffman", [False, True])
+def test_encode_blocks_match_restatement(huffman):
+    """hpk_henc_encode_blocks on the CPU batch path against the encoder.rs restatement
+    (oracle/hpack_ref.Encoder; encoder.rs:210-234, string literals encoder.rs:296-307 with the H bit
+    when shorter) block by block, on interop lists plus random binary and numeric values."""
+    lists = response_lists(seed=5)
+    k = 5
+    encs = [hpack.Encoder(huffman=huffman) for _ in range(k)]
+    refs = [hpack_ref.Encoder(huffman=huffman) for _ in range(k)]
+    got = hpack.encode_blocks([(encs[i % k], hs) for i, hs in enumerate(lists)], None)
+    want = [refs[i % k].encode(hs) for i, hs in enumerate(lists)]
+    assert got == want
+
+
+@pytest.mark.parametrize("huffman", [False, True])
+def test_failed_encode_blocks_leaves_encoders_unchanged(huffman):
+    """A batch call that fails after the table pass (here: an injected Huffman-batch failure) must
+    leave every encoder's dynamic table as it was (hpk_henc_encode's copy-and-commit): the next call
+    gives the bytes fresh encoders give for the same blocks."""
+    L = _lib.lib()
+    lists = response_lists(seed=11, n=300)
+    k = 3
+    encs = [hpack.Encoder(huffman=huffman) for _ in range(k)]
+    warm = lists[:30]
+    hpack.encode_blocks([(encs[i % k], hs) for i, hs in enumerate(warm)], None)
+    refs = [hpack_ref.Encoder(huffman=huffman) for _ in range(k)]
+    for i, hs in enumerate(warm):
+        refs[i % k].encode(hs)
+    rest = lists[30:]
+    pairs = [(encs[i % k], hs) for i, hs in enumerate(rest)]
+    if huffman:  # the injected failure sits in the Huffman batch, which only Huffman encoders make
+        L.hpk_test_fail_batches(1)
+        try:
+            with pytest.raises(RuntimeError, match="injected"):
+                hpack.encode_blocks(pairs, None)
+        finally:
+            L.hpk_test_fail_batches(0)
+    got = hpack.encode_blocks(pairs, None)
+    assert got == [refs[i % k].encode(hs) for i, hs in enumerate(rest)]
