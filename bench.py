@@ -55,20 +55,33 @@ def parse():
     ap.add_argument("--workload", choices=["config5", "config2"], default="config5")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 side measurement")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 encode/decode side measurement")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 captured-HEADERS side measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the scatter+decode+gather leg (N > 1)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this GPU's host-CPU share (<= 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU of this process's affinity mask, capped at the GPU's host-CPU share (16)")
     ap.add_argument("--pmc-dir", default=os.path.join(REPO, "profiles"))
     return ap.parse_args()
 
 
-def cpu_threads(arg):
-    if arg > 0:
-        return arg
+def affinity_cpus():
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except Exception:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))  # the GPU box allots 16 host CPUs per GPU
+        return os.cpu_count() or 1
+
+
+HOST_CPU_SHARE = 16  # the GPU box allots 16 host CPUs per GPU (its OMP_NUM_THREADS / MAX_JOBS)
+
+
+def cpu_threads(arg):
+    """Threads for the CPU baselines: --cpu-threads, else every CPU of the affinity mask, capped at
+    the GPU's host-CPU share (the box's mask can list the whole machine, of which one GPU's job owns
+    16 CPUs). Returns (threads, affinity count)."""
+    aff = affinity_cpus()
+    if arg > 0:
+        return arg, aff
+    return max(1, min(HOST_CPU_SHARE, aff)), aff
 
 
 def cpu_model():
@@ -155,17 +168,40 @@ def make_unit(codec, w, dev, copies=1):
     return sets
 
 
-def pmc_traffic(path, workload, literals, version):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary of this exact workload and
-    kernel build (scripts/pmc_traffic.py); None when there is none."""
+def source_hash():
+    """sha256 (16 hex digits) of the library's sources (loona_amd/csrc + include/hpk.h): the key of
+    the committed PMC summaries, so a kernel change invalidates them whether or not anyone edits a
+    version string."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(REPO, "loona_amd", "csrc")
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".h", ".hip", ".cpp")) or f == "Makefile")
+    for f in names:
+        h.update(f.encode())
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(REPO, "include", "hpk.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_summary(path, workload, literals, src):
+    """A committed rocprofv3 PMC summary of this exact workload and library source (scripts/
+    pmc_traffic.py, scripts/pmc_sq.py); None when there is none."""
     try:
         with open(path) as f:
             pm = json.load(f)
-        if pm.get("workload") == workload and pm.get("literals") == literals and pm.get("kernel_version") == version:
-            return pm.get("hbm_bytes_per_launch")
+        if pm.get("workload") == workload and pm.get("literals") == literals and pm.get("src_sha16") == src:
+            return pm
     except Exception:
         pass
     return None
+
+
+def pmc_traffic(path, workload, literals, src):
+    pm = pmc_summary(path, workload, literals, src)
+    return pm.get("hbm_bytes_per_launch") if pm else None
 
 
 def time_launches(codec, sets, stream, steps, warmup):
@@ -186,6 +222,121 @@ def time_launches(codec, sets, stream, steps, warmup):
     ev1.record(stream)
     torch.cuda.synchronize()
     return ev0.elapsed_time(ev1) / 1e3
+
+
+def cuda_time(fn, reps, stream):
+    """Seconds per call of fn (device work on `stream`), HIP events around reps back-to-back calls."""
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def run_config3(codec, stream, dev, reps=10):
+    """BASELINE config 3: 1M mixed literals (Zipf(1.1) lengths 8..4096, 5 % uniform bytes), device
+    encode and device decode timed apart, each over `reps` back-to-back launches; the round trip is
+    bit-exact (every decoded byte equals the generated strings; the encode into hpk_encoded_bound
+    regions equals the exact-size encode the decode consumed, whose lengths equal the sums of the
+    RFC 7541 code lengths)."""
+    import torch
+
+    from loona_amd import synth
+    from loona_amd.batch import decode_offsets_torch, encode_offsets_torch
+
+    w = synth.device_config3(codec, 1_000_000, device=dev)
+    n = w.n
+    doff32 = w.dec_off.to(torch.int32)
+    eoff = encode_offsets_torch(doff32)
+    e_out = torch.empty((int(eoff[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device=dev)
+    e_len = torch.empty(n, dtype=torch.int32, device=dev)
+    e_st = torch.empty(n, dtype=torch.uint8, device=dev)
+    t_enc = cuda_time(lambda: codec.encode_into(w.dec_blob, doff32, e_out, eoff, e_len, e_st, device=True), reps,
+                      stream)
+    ok_enc = (not e_st.any().item()) and bool(torch.equal(
+        synth.gather_output(e_out, eoff, e_len, 0, n), w.enc_blob[: w.enc_bytes]))
+    doff = decode_offsets_torch(w.enc_off)
+    d_out = torch.empty((int(doff[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device=dev)
+    d_len = torch.empty(n, dtype=torch.int32, device=dev)
+    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
+    t_dec = cuda_time(lambda: codec.decode_into(w.enc_blob, w.enc_off, d_out, doff, d_len, d_st, device=True), reps,
+                      stream)
+    synth.check_decoded(w, d_out, doff, d_len, d_st)  # raises on any difference
+    algo = w.enc_bytes + w.dec_bytes + 13 * n
+    return {"literals": n, "decoded_bytes": w.dec_bytes, "encoded_bytes": w.enc_bytes,
+            "decode_us": round(t_dec * 1e6, 2), "decode_GiB_s_of_input": round(w.enc_bytes / t_dec / 2**30, 2),
+            "decode_roofline_frac": round(algo / t_dec / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_us": round(t_enc * 1e6, 2), "encode_GiB_s_of_input": round(w.dec_bytes / t_enc / 2**30, 2),
+            "encode_roofline_frac": round(algo / t_enc / 1e9 / HBM_PEAK_GBS, 4),
+            "round_trip_bit_exact": True, "encode_matches_exact_region_encode": ok_enc,
+            "note": f"device-generated, {reps} back-to-back launches per kernel; algorithmic bytes enc + dec + 13 "
+                    "per literal for both kernels"}
+
+
+def run_config4(codec, threads):
+    """BASELINE config 4: captured HEADERS — the interop stories' header blocks (five encoders' real
+    output, crates/loona-hpack/fixtures/hpack/interop) replicated to >= 1M Huffman literals, one
+    hpk_hdec per connection (a story), decoded by ONE hpk_hdec_decode_blocks call: host span walk,
+    one Huffman batch (device, from host buffers: H2D + kernel + D2H), in-order apply; against the
+    same call on the library's CPU batch path. Host-inclusive, wall clock, the second of two calls."""
+    import ctypes
+    import gzip
+
+    from loona_amd import _lib
+
+    gold = os.path.join(REPO, "tests", "golden")
+    with gzip.open(os.path.join(gold, "interop.json.gz"), "rt") as f:
+        inter = json.load(f)
+    with open(os.path.join(gold, "interop_digest.json")) as f:
+        dig = json.load(f)
+    stories = [[bytes.fromhex(c["wire"]) for c in st["cases"]] for enc in sorted(inter) for st in inter[enc]]
+    reps = -(-1_000_000 // dig["huffman_literals"])
+    L = _lib.lib()
+    blocks, owners = [], []
+    for r in range(reps):
+        for si, st in enumerate(stories):
+            for b in st:
+                blocks.append(b)
+                owners.append(r * len(stories) + si)
+    nconn = reps * len(stories)
+    off = np.zeros(len(blocks) + 1, np.int64)
+    np.cumsum([len(b) for b in blocks], out=off[1:])
+    blob = np.frombuffer(b"".join(blocks), np.uint8).copy()
+    off32 = off.astype(np.uint32)
+    res = {}
+    for leg, ctx in (("device", codec._h), ("cpu_batch", None)):
+        for _ in range(2):  # the first call grows the context's scratch buffers: time the second
+            decs = [L.hpk_hdec_create() for _ in range(nconn)]
+            arr = (ctypes.c_void_p * len(blocks))(*[decs[o] for o in owners])
+            out = _lib.BlocksOut()
+            t0 = time.perf_counter()
+            rc = L.hpk_hdec_decode_blocks(ctx, arr, blob.ctypes.data, off32.ctypes.data, len(blocks), ctypes.byref(out))
+            dt = time.perf_counter() - t0
+            _lib.check(rc, "hpk_hdec_decode_blocks")
+            errs = sum(1 for b in range(len(blocks)) if out.blocks[b].error)
+            nh = out.n_headers
+            L.hpk_blocks_out_free(ctypes.byref(out))
+            for d in decs:
+                L.hpk_hdec_destroy(d)
+        res[leg] = (dt, errs, nh)
+    lit_bytes = dig["encoded_bytes"] * reps
+    return {"source": "crates/loona-hpack/fixtures/hpack/interop (5 encoders' captured header blocks)",
+            "connections": nconn, "header_blocks": len(blocks), "huffman_literals": dig["huffman_literals"] * reps,
+            "huffman_bytes": lit_bytes, "headers": res["device"][2], "block_errors": res["device"][1],
+            "device_ms": round(res["device"][0] * 1e3, 2), "cpu_batch_ms": round(res["cpu_batch"][0] * 1e3, 2),
+            "device_blocks_per_s": round(len(blocks) / res["device"][0], 1),
+            "cpu_batch_blocks_per_s": round(len(blocks) / res["cpu_batch"][0], 1),
+            "device_over_cpu": round(res["cpu_batch"][0] / res["device"][0], 3),
+            "host_threads": threads,
+            "note": "host-inclusive wall clock of one hpk_hdec_decode_blocks call: span walk, Huffman batch "
+                    "(device: from host buffers, H2D + kernel + D2H), in-order apply with each connection's "
+                    "dynamic table"}
 
 
 def main():
@@ -336,8 +487,25 @@ def main():
         algo_per_launch = algo_local / launches_per_step
         achieved = algo_per_launch / per_launch_s / 1e9
         lit_per_launch = my_n // launches_per_step if args.workload == "config5" else units[0][0].n
-        traffic = pmc_traffic(os.path.join(args.pmc_dir, f"pmc_{args.workload}.json"), args.workload,
-                              lit_per_launch, version)
+        src = source_hash()
+        pm_hbm = pmc_summary(os.path.join(args.pmc_dir, f"pmc_{args.workload}.json"), args.workload, lit_per_launch,
+                             src)
+        traffic = pm_hbm.get("hbm_bytes_per_launch") if pm_hbm else None
+        pm_sq = pmc_summary(os.path.join(args.pmc_dir, f"pmc_sq_{args.workload}.json"), args.workload,
+                            lit_per_launch, src)
+        issue = None
+        if pm_sq:
+            per = pm_sq["per_launch"]
+            issue = {"valu_insts_per_launch": per.get("SQ_INSTS_VALU"),
+                     "lds_insts_per_launch": per.get("SQ_INSTS_LDS"),
+                     "lds_active_cycles_per_launch": per.get("SQ_LDS_IDX_ACTIVE"),
+                     "source": f"profiles/pmc_sq_{args.workload}.json (src_sha16 {src})",
+                     "basis": "this run's avg launch time, 2.4 GHz; VALU: 2 cycles per wave64 instruction on each "
+                              "of 1,024 SIMD-32s; LDS: LDS-array cycles of 256 CUs"}
+            if per.get("SQ_INSTS_VALU"):
+                issue["valu_frac"] = round(per["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9 * per_launch_s), 4)
+            if per.get("SQ_LDS_IDX_ACTIVE"):
+                issue["lds_frac"] = round(per["SQ_LDS_IDX_ACTIVE"] / (256 * 2.4e9 * per_launch_s), 4)
         line = {
             "metric": METRIC,
             "value": round(all_enc * args.steps / t_max / 2**30, 3),
@@ -372,12 +540,16 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_read": pm_hbm.get("read_bytes_per_launch") if pm_hbm else None,
+                "traffic_write": pm_hbm.get("write_bytes_per_launch") if pm_hbm else None,
+                "issue": issue,
                 "kernel": "hpk_decode12",
                 "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "literals_per_launch": int(lit_per_launch),
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
             },
             "kernel_version": version,
+            "src_sha16": source_hash(),
         }
         if e2e is not None:
             line["e2e_scatter_decode_gather"] = e2e
@@ -398,15 +570,24 @@ def main():
             "value": round(w2.enc_bytes * k2 / t2 / 2**30, 3), "unit": "GiB/s", "literals": w2.n,
             "encoded_bytes": w2.enc_bytes, "avg_launch_us": round(t2 / k2 * 1e6, 3),
             "algorithmic_bytes_per_launch": a2, "roofline_frac": round(a2 / (t2 / k2) / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(os.path.join(args.pmc_dir, "pmc_config2.json"), "config2", w2.n, version),
+            "traffic": pmc_traffic(os.path.join(args.pmc_dir, "pmc_config2.json"), "config2", w2.n, source_hash()),
             "note": "1M literals, 4 rotating input/output copies (> 256 MiB Infinity Cache), 100 launches"}
         cpu_w = w2
     elif rank == 0:
         cpu_w = units[0][0]
+    if rank == 0 and args.workload == "config5" and not args.no_config3:
+        line["config3"] = run_config3(codec, stream, dev)
+        torch.cuda.empty_cache()
+    if rank == 0 and args.workload == "config5" and not args.no_config4:
+        line["config4"] = run_config4(codec, cpu_threads(args.cpu_threads)[0])
     if rank == 0 and not args.no_cpu:
         blob_h = cpu_w.enc_blob.cpu().numpy()
         off_h = cpu_w.enc_off.cpu().numpy().view(np.uint32).copy()
-        base, fast = run_cpu_baselines(blob_h, off_h, cpu_threads(args.cpu_threads))
+        th, aff = cpu_threads(args.cpu_threads)
+        base, fast = run_cpu_baselines(blob_h, off_h, th)
+        base["affinity_cpus"] = aff
+        base["threads_rule"] = (f"every CPU of the affinity mask ({aff}) capped at this GPU's host-CPU share "
+                                f"({HOST_CPU_SHARE}): {th} threads")
         line["cpu_baseline"] = base
         line["cpu_fast"] = fast
     if rank == 0:

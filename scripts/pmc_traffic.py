@@ -25,9 +25,12 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 mean = {k: sum(v) / len(v) for k, v in vals.items()}
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402
 from loona_amd import _lib  # noqa: E402
 
-out = {"kernel": kname, "workload": workload, "kernel_version": _lib.lib().hpk_version().decode(), "literals": literals, "dispatches": {k: len(v) for k, v in vals.items()}, "raw_mean": mean}
+out = {"kernel": kname, "workload": workload, "kernel_version": _lib.lib().hpk_version().decode(),
+       "src_sha16": bench.source_hash(), "literals": literals, "dispatches": {k: len(v) for k, v in vals.items()},
+       "raw_mean": mean}
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     rd = mean["FETCH_SIZE"] * 1024 * 2
     wr = mean["WRITE_SIZE"] * 1024
