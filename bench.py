@@ -478,7 +478,8 @@ def main():
             e2e = {"value": round(enc_total / dt / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 3),
                    "steps": reps, "statuses_ok": bool(ok),
                    "what": "rank 0 holds the 8 shards; RCCL grouped send/recv of offsets + blob to each owner, "
-                           "device decode, RCCL send/recv of out_blob/out_off/out_len/status back; no host copy"}
+                           "device decode, the decoded bytes laid end to end on the owner, one all-reduce of the "
+                           "decoded sizes, RCCL send/recv of bytes/out_len/status back; no host copy of the data"}
         del res, shards
 
     line = None

@@ -10,7 +10,7 @@
 #include <vector>
 
 #include "legacy_decode11.h"
-#include "../loona_amd/csrc/hpk_decode12.h"
+#include "legacy_decode12.h"
 
 using namespace hpkdec;
 

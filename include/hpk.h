@@ -125,6 +125,15 @@ int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
                      uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                      uint8_t* status, int flags);
 
+/* Which decode kernel a context's batches use. Both give identical results (the parity tests run
+ * every case through each); they differ in speed by batch size. HPK_DECODE_AUTO (the default): the
+ * wave-fill kernel (decode v25) for batches of at least 4M literals, the workgroup-fill kernel
+ * (v24) below that. */
+#define HPK_DECODE_AUTO 0
+#define HPK_DECODE_FILL 1 /* workgroup fills: one fill at a time per CU, barriers between fills */
+#define HPK_DECODE_WAVE 2 /* wave fills: every wave its own fills, no barriers between them */
+int hpk_ctx_set_decode_kernel(hpk_ctx* ctx, int kind);
+
 /* Read and clear the context's sticky device error flag (after HPK_ASYNC calls; synchronises the
  * ctx stream). Returns HPK_E_OK, HPK_E_INVAL (some call saw bad offsets) or HPK_E_DEVICE.
  * The flag belongs to the context, not to a stream: it reports a bad call made on any stream the

@@ -79,6 +79,7 @@ EXPORTS = (
     "hpk_henc_encode_blocks",
     "hpk_henc_out_free",
     "hpk_test_fail_batches",
+    "hpk_ctx_set_decode_kernel",
     "hpk_version",
 )
 
@@ -224,6 +225,8 @@ def lib() -> ctypes.CDLL:
         L.hpk_henc_encode_blocks.restype = ctypes.c_int
         L.hpk_henc_out_free.argtypes = [ctypes.POINTER(HencOut)]
         L.hpk_henc_out_free.restype = None
+        L.hpk_ctx_set_decode_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.hpk_ctx_set_decode_kernel.restype = ctypes.c_int
         L.hpk_test_fail_batches.argtypes = [ctypes.c_int]
         L.hpk_test_fail_batches.restype = None
         L.hpk_version.argtypes = []

@@ -159,6 +159,12 @@ extern "C" int hpk_host_unregister(void* ptr) {
     return HPK_E_OK;
 }
 
+extern "C" int hpk_ctx_set_decode_kernel(hpk_ctx* c, int kind) {
+    if (!c || kind < HPK_DECODE_AUTO || kind > HPK_DECODE_WAVE) return hpk_set_err_msg("bad decode kernel", HPK_E_INVAL);
+    c->decode_kernel = kind;
+    return HPK_E_OK;
+}
+
 extern "C" void* hpk_ctx_stream(hpk_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 extern "C" int hpk_ctx_sync(hpk_ctx* c) {

@@ -5,76 +5,51 @@
 // (crates/loona-hpack/src/huffman.rs:95-161), with identical results per literal: decoded bytes,
 // and status Ok / PaddingTooLarge / InvalidPadding / EOSInString with the reference's precedence.
 //
-// Work decomposition (kernel template hpk_decode12 in hpk_decode12.h):
-//   * one 1024-thread workgroup per CU (16 waves) owns a contiguous literal range (n / CUs); the
-//     decode tables (16 KiB two-symbol table, 1.9 KiB leading-ones table) are staged into LDS once;
-//   * the range is decoded in fills: a 40 KiB LDS input window (big-endian dwords), an LDS image
-//     of the fill's output span and a queue of up to 2048 literals ordered longest-first (counting
-//     sort on the encoded length). The next fill's offsets and window are loaded into registers
-//     while the current fill decodes, the previous fill's image is written back with 16-byte
-//     stores while it decodes; barriers order LDS only;
-//   * literals of >= 224 encoded bytes (the queue's head) are decoded one per wave, cooperatively:
-//     64 lanes walk 64 segments from speculative starts and re-walk from their neighbours' true
-//     stops until nothing changes (Huffman walks resynchronise within a few codes);
-//   * the other literals are decoded one per lane out of LDS in a static snake over the
-//     longest-first queue: lane i takes slots i and 2*1024-1-i (the longest with the shortest),
-//     the second literal's entry and first window dwords read while the first one decodes, so a
-//     lane moves on without waiting for LDS;
-//   * a step is two lookups in the 12-bit two-symbol table, each decoding up to two codes of
-//     <= 12 bits, from a 32-bit window made by ONE v_alignbit out of a register-held dword pair;
-//     a code longer than 12 bits (or EOS) takes one leading-ones lookup (any code in one read).
-//     Bits past a literal's end are NOT masked: a code that runs past the end is, by
-//     prefix-freeness, longer than what is left whatever follows, so the walk stops exactly where
-//     huffman.rs's bit iterator stops matching; only the final padding check (huffman.rs:128-160)
-//     looks at the residual bits;
-//   * a literal whose output capacity is below hpk_decoded_bound (caller-chosen offsets) is decoded
-//     after the queue drains, code by code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
-// A literal too large for the window is decoded by one lane straight from global memory.
+// Two kernels, identical results (tests/test_gpu.py runs every case through both):
+//   * hpk_decode_wave (v25, hpk_wave.h), for large batches: every wave of a 1024-thread workgroup
+//     decodes its own fills of <= 128 literals (two per lane, longest with shortest) out of its own
+//     LDS window into its own LDS image, with no barrier between fills, so the waves' memory traffic
+//     and setup overlap each other's decoding; the workgroup's range is handed out in chunks;
+//   * hpk_decode12 (v24, hpk_decode12.h), for small batches: one workgroup-wide fill at a time per
+//     CU (40 KiB window, 77 KiB image, 2048-literal longest-first queue), the next fill's loads in
+//     flight during the decode, the previous image written back around it.
+// Both use the same lane walk (hpk_decode12.h): a step is two lookups in the 12-bit two-symbol
+// table, each decoding up to two codes of <= 12 bits, from a 32-bit window made by ONE v_alignbit
+// out of a register-held dword pair; a longer code (or EOS) takes one leading-ones lookup. Bits past
+// a literal's end are not masked: a code that runs past the end is, by prefix-freeness, longer than
+// what is left whatever follows, so the walk stops exactly where huffman.rs's bit iterator stops
+// matching; only the final padding check (huffman.rs:128-160) looks at the residual bits. Literals
+// of >= 64 encoded bytes go to the long-literal phase (hpk_long.h), one lane each streaming from
+// HBM, after the fills; a literal whose output region is below hpk_decoded_bound is decoded code by
+// code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
 #include <stdlib.h>
 
-#include "hpk_decode12.h"
+#include "hpk_wave.h"
 
 using namespace hpkdec;
 
-// Product geometry (v12): 16 waves (one 1024-thread workgroup) per CU; per fill a 40 KiB input
-// window, a 77 KiB output image and a 2048-entry longest-first queue, plus the 16 KiB two-symbol
-// table; two lookups per step, lanes check for a finished literal every 2 steps, static snake
-// schedule, byte stores into the image (bench/kvariants: profiles/r01/kvariants_v1[23]*.jsonl).
-#ifndef HPK_REFILLN
-#define HPK_REFILLN 2  // lane steps between two finish checks
-#endif
-constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = HPK_REFILLN, kChunk = 64, kLook = 2, kSched = 1;
-constexpr bool kAcc = false;
-constexpr int kCoop = 0;  // (v16: literals of >= 224 encoded bytes one wave each; v19: hpk_decode_long)
-#ifndef HPK_LONGK
-#define HPK_LONGK 1
-#endif
-#ifndef HPK_SPREAD
-#define HPK_SPREAD 0
-#endif
-constexpr int kLongK = HPK_LONGK;  // long literals left to the long-literal phase (hpk_long.h)
-constexpr int kSpread = HPK_SPREAD;  // lane-queue slots interleaved over the waves (fills of few literals use every SIMD)
+// Workgroup-fill kernel (v24, hpk_decode12.h): 16 waves (one 1024-thread workgroup) per CU; per
+// fill a 40 KiB input window, a 77 KiB output image and a 2048-entry longest-first queue, plus the
+// 16 KiB two-symbol table; lanes check for a finished literal every 2 steps.
+constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2;
+// long-literal phase (hpk_long.h, both kernels): literals of >= HPK_LONG_MIN encoded bytes, those of
+// >= HPK_LONG_BIG first (longest-first, roughly)
 #ifndef HPK_LONG_MIN
-#define HPK_LONG_MIN 64  // encoded bytes: literals from here on go to the long-literal phase
+#define HPK_LONG_MIN 64
 #endif
 #ifndef HPK_LONG_BIG
-#define HPK_LONG_BIG 1024  // the long-literal phase takes these first (longest-first, roughly)
+#define HPK_LONG_BIG 1024
 #endif
 using Geo = Geo12<kWaves, kW, kO, kQ>;
-#ifndef HPK_LONGDYN
-#define HPK_LONGDYN 1
+// Wave-fill kernel (v25, hpk_wave.h): per wave a 3 KiB window and a 5.75 KiB image, the workgroup's
+// range handed out in chunks of 224 literals; for batches of at least HPK_WAVE_MIN literals (smaller
+// ones keep the workgroup-fill kernel) unless the context says otherwise (hpk_ctx_set_decode_kernel)
+constexpr int kWaveWin = 3072, kWaveImg = 5888;
+#ifndef HPK_WAVE_MIN
+#define HPK_WAVE_MIN 4000000u
 #endif
-#ifndef HPK_DEFER
-#define HPK_DEFER 0
-#endif
-constexpr int kLongDyn = HPK_LONGDYN;     // long literals: waves take the next one from an LDS counter
-constexpr int kDefer = HPK_DEFER;  // the previous fill's write-back issued during this decode
-#ifndef HPK_PREDST
-#define HPK_PREDST 1
-#endif
-constexpr int kPredSt = HPK_PREDST;  // unconditional byte stores in the lane step (dummy slots)
-#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN, kChunk, kLook, kAcc, kCoop, kSched, kLongDyn, kDefer, kPredSt, \
-                                   kSpread, 512, 0, 1, 15, 32, kLongK>
+#define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, 224u>
+#define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN>
 
 #ifdef HPK_DIAG
 // Diagnostic build (libhpk_diag.so, `make diag`; never the product library): HPK_DEBUG_MODE selects
@@ -132,10 +107,31 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
+    bool wave = c->decode_kernel == HPK_DECODE_WAVE || (c->decode_kernel == HPK_DECODE_AUTO && b.n >= HPK_WAVE_MIN);
 #ifdef HPK_DIAG
+    if (const char* wk = getenv("HPK_DECODE_KERNEL")) wave = wk[0] == 'w';  // "wave" / "fill" (A/B runs)
     if (g_debug_mode < 0) {
         const char* dm = getenv("HPK_DEBUG_MODE");
         g_debug_mode = dm ? atoi(dm) : 0;
+    }
+    if (wave) {
+        if (g_debug_mode == 1) {
+            hipLaunchKernelGGL(WAVE_KERNEL(1), grid, block, 0, c->stream, a);
+        } else if (g_debug_mode == 3) {
+            const size_t need = (size_t)blocks * kWaves * 16;
+            if (need > g_dbg_n) {
+                (void)hipFree(g_dbg);
+                HIP_TRY(hipMalloc(&g_dbg, need * 8));
+                g_dbg_n = need;
+            }
+            a.dbg = g_dbg;
+            hipLaunchKernelGGL(WAVE_KERNEL(3), grid, block, 0, c->stream, a);
+        } else if (g_debug_mode == 2)
+            hipLaunchKernelGGL(WAVE_KERNEL(2), grid, block, 0, c->stream, a);
+        else
+            hipLaunchKernelGGL(WAVE_KERNEL(0), grid, block, 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        return hpk_long_list_used(c, lslot);
     }
     switch (g_debug_mode) {
         case 1:
@@ -174,7 +170,10 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
             hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
     }
 #else
-    hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
+    if (wave)
+        hipLaunchKernelGGL(WAVE_KERNEL(0), grid, block, 0, c->stream, a);
+    else
+        hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
 #endif
     HIP_TRY(hipGetLastError());
     return hpk_long_list_used(c, lslot);

@@ -12,6 +12,7 @@
 struct hpk_ctx {
     int device = 0;
     int num_cu = 256;
+    int decode_kernel = HPK_DECODE_AUTO;  // hpk_ctx_set_decode_kernel
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     uint32_t* d_lut = nullptr;

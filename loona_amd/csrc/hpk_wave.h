@@ -1,0 +1,498 @@
+// hpk_wave.h — decode v25: wave fills. Every wave of the workgroup decodes its own contiguous
+// literal range in fills of at most 128 literals (two per lane) with no workgroup barrier between
+// the fills, so one wave's memory traffic and setup overlap the other fifteen waves' decoding.
+//
+// Why (profiles/r03/decomposition_v24_modes.jsonl): the v24 fill kernel spends 631 of its 1,178 us
+// per 32M-literal launch in the fill machinery alone (decode switched off), because all 16 waves of
+// a workgroup set up, wait at the fill-top barrier for the fill's slowest literal and write back
+// together, so the CU's memory path and its LDS/VALU take turns instead of overlapping. A lane
+// stream per lane (each lane its own literal range) was ruled out by profiles/r03/
+// ta_probe_lane_vs_coalesced.jsonl: 16-byte stores to 64 addresses per instruction run at 45 % of
+// the coalesced rate. Here every transfer is still a coalesced wave-wide piece (window loads,
+// image write-back, offsets), and every wave runs its own pipeline:
+//   * per wave an input window (kWinB bytes, big-endian dwords) and an output image (kImgB bytes,
+//     the last 256 the lanes' dummy slots) in LDS; the 16 waves' areas plus the shared tables fill
+//     the CU's 160 KiB;
+//   * a fill is the longest prefix of the next 128 literals whose input fits the window and whose
+//     output regions fit the image; its offsets and window were loaded into registers while the
+//     previous fill decoded;
+//   * per fill: the offsets are checked (decoder.rs:138-142: a literal's bounds before any Huffman
+//     work), the previous fill's image and lengths are written back, the fill's literals are sorted
+//     longest-first by a per-wave counting sort (LDS atomics on 32 length classes, in the image),
+//     the window is staged and the next fill's loads are issued; then lane i decodes queue slots i
+//     and 127 - i (the static snake of v13: the longest with the shortest, both read before the
+//     first step) with the two-lookup step of v12 (lit12_step), unconditional byte stores of v14 and
+//     the late length/status of v22;
+//   * literals of >= long_min encoded bytes whose region holds the decoded bound are listed for the
+//     long-literal phase (hpk_long.h) after all waves are done, as v19 did; a workgroup range made
+//     mostly of them (config 3) is listed whole without any wave fill;
+//   * a literal whose region is below the decoded bound is decoded code by code with a capacity
+//     check per byte by the lane that holds it, after the lane loop (HPK_OUTPUT_OVERFLOW);
+//   * bad offsets stop the wave (HPK_BAD_OFFSETS for the rest of its range) and, through an LDS flag
+//     read at every fill, the workgroup's other waves at their next fill.
+// Semantics are huffman.rs:95-161 through lit12_step (hpk_decode12.h).
+#pragma once
+#include "hpk_decode12.h"
+
+namespace hpkdec {
+
+template <int kWinB, int kImgB>
+struct GeoW {
+    static constexpr int kWaves = 16, kBlock = kWaves * 64;
+    static constexpr int kWaveBytes = kWinB + kImgB;
+    static constexpr int kLutOff = kTabBytes;                    // T8 + LO (kTabBytes), then LUT2
+    static constexpr int kWaveOff = kTabBytes + (int)HPK_LUT_SIZE * 4;
+    static constexpr int kCtrOff = kWaveOff + kWaves * kWaveBytes;
+    static constexpr int kLdsBytes = kCtrOff + 64;
+    static constexpr int kImg = kImgB - 256;                     // usable image bytes (dummy slots after)
+    static constexpr int kWinRounds = (kWinB / 16 + 63) / 64;    // window chunks per lane
+    static constexpr int kFlushRounds = (kImg / 16 + 1 + 63) / 64;
+    static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
+    static_assert(kWinB % 16 == 0 && kImgB % 16 == 0 && kWinB < 65536 && kImgB < 131072, "entry packing");
+    // the long-literal phase's rings and queues (hpk_long.h) over the wave areas after the fills
+    static_assert(kWaves * kWaveBytes >= 512 * (32 * 4 + HPK_LONG_OS) + 8 * 128 * 16, "long-phase LDS");
+};
+
+// WG counters (s_ctr): [0] bad offsets seen (waves stop at their next fill), [1] long list, front
+// (>= long_big bytes), [2] long list, back, [3] long-phase claim, [4]/[5] dense check sums, [6] the
+// dense listing found an entry it cannot list, [7] chunks of kChunk literals handed out to the waves
+template <int kMode, int kWinB, int kImgB, uint32_t kChunk>
+__global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
+    using G = GeoW<kWinB, kImgB>;
+    constexpr int kStore = kMode == 2 ? kNoStore : kPred;
+    // kMode 3 (diagnostic builds): per-wave cycle stamps into a.dbg[wave * 16 + i]: 0 total, 1 waiting
+    // for the fill's offsets + their checks, 2 write-back, 3 queue, 4 window staging, 5 prefetch issue
+    // and queue reads, 6 lane loop, 7 byte path + results, 8 fills, 9 lane-loop rounds, 10 long phase,
+    // 11 before the first fill
+    unsigned long long dg[12] = {};
+    unsigned long long tq = kMode == 3 ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long t_start = tq;
+    auto stamp = [&](int i) {
+        if (kMode == 3) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            dg[i] += t - tq;
+            tq = t;
+        }
+    };
+    constexpr int R = G::kWinRounds, F = G::kFlushRounds;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[G::kLdsBytes];
+    uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
+    uint32_t* s_lut = reinterpret_cast<uint32_t*>(smem + G::kLutOff);
+    uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+    for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut2)[t];
+    if (tid < 16) s_ctr[tid] = 0;
+    const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
+    const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+    const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
+    const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
+    auto leave = [&](uint32_t i, uint32_t nb) {  // list literal i for the long-literal phase
+        if (nb >= a.long_big)
+            a.long_list[BA + atomicAdd(&s_ctr[1], 1u)] = i;
+        else
+            a.long_list[BB - 1u - atomicAdd(&s_ctr[2], 1u)] = i;
+    };
+    __syncthreads();
+    // ---- a range whose first literals hold mostly long-literal bytes (config 3) is listed whole ----
+    bool dense = false;
+    {
+        const uint32_t k = min(BB - BA, 2048u);
+        uint32_t dlb = 0, dtb = 0;
+        for (uint32_t t = tid; t < k; t += G::kBlock) {
+            const uint32_t nb = min(a.in_off[BA + t + 1] - a.in_off[BA + t], 1u << 20);  // (bad offsets: bounded)
+            dtb += nb;
+            dlb += nb >= a.long_min ? nb : 0u;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            dlb += __shfl_xor(dlb, d);
+            dtb += __shfl_xor(dtb, d);
+        }
+        if (lane == 0 && dtb) {
+            atomicAdd(&s_ctr[4], dlb);
+            atomicAdd(&s_ctr[5], dtb);
+        }
+        __syncthreads();
+        if (s_ctr[4] > s_ctr[5] / 2u) {  // block-uniform
+            bool no = false;
+            for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
+                const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q0 = a.out_off[i], q1 = a.out_off[i + 1];
+                const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
+                                (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
+                if (ok)
+                    leave(i, p1 - p0);
+                else
+                    no = true;
+            }
+            if (__any(no) && lane == 0) s_ctr[6] = 1u;
+            __syncthreads();
+            dense = s_ctr[6] == 0u;
+            if (!dense) {  // not all listable: the range goes through the wave fills after all
+                __syncthreads();
+                if (tid == 0) {
+                    s_ctr[1] = 0;
+                    s_ctr[2] = 0;
+                }
+                __syncthreads();
+            }
+        }
+    }
+    if (!dense) {
+        // ---- wave fills ----
+        uint8_t* const s_win = smem + G::kWaveOff + wv * G::kWaveBytes;
+        uint8_t* const s_img = s_win + kWinB;
+        const uint32_t* const win32 = reinterpret_cast<const uint32_t*>(s_win);
+        const uint32_t dmy = (uint32_t)G::kImg + lane * 4u;
+        // The workgroup's range is handed out in chunks of kChunk literals (about two fills), in order,
+        // to whichever wave asks next (an LDS counter): a static split left the waves the SIMDs'
+        // arbitration favours idle at the end while the others finished (11 % of a wave's time).
+        // A wave holds its current chunk and has already claimed the next one, whose first offsets are
+        // loaded a fill ahead of their use.
+        auto claim = [&](uint32_t& ca, uint32_t& ce) {
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(&s_ctr[7], 1u);
+            c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+            const uint64_t lo = (uint64_t)BA + (uint64_t)c * kChunk;
+            ca = (uint32_t)min(lo, (uint64_t)BB);
+            ce = (uint32_t)min(lo + kChunk, (uint64_t)BB);
+        };
+        // registers of the next fill: offsets of slots lane and lane + 64, the window chunks
+        uint32_t io0[2], io1[2], oo0[2], oo1[2];
+        uint4 ch[R];
+        auto prefetch = [&](uint32_t c, uint32_t e, uint32_t base16) {
+            const uint32_t cnt = min(128u, e - c);  // >= 1
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t t = c + min(lane + 64u * r, cnt - 1u);
+                io0[r] = a.in_off[t];
+                io1[r] = a.in_off[t + 1];
+                oo0[r] = a.out_off[t];
+                oo1[r] = a.out_off[t + 1];
+            }
+            const uint4* g16 = reinterpret_cast<const uint4*>(a.in_base);
+#pragma unroll
+            for (int r = 0; r < R; ++r) ch[r] = g16[min((base16 >> 4) + lane + 64u * r, last16)];
+        };
+        uint32_t cur, ce, na, ne;
+        claim(cur, ce);
+        claim(na, ne);
+        uint32_t gin = 0, gout = 0, ngin = 0, ngout = 0;
+        if (cur < ce) {
+            gin = a.in_off[cur] + a.in_mis;
+            gout = a.out_off[cur] + a.out_mis;
+            prefetch(cur, ce, gin & ~15u);
+        }
+        if (na < ne) {
+            ngin = a.in_off[na];
+            ngout = a.out_off[na];
+        }
+        // the previous fill, not yet written back: literals [pcur, pcur + pk), output [pG0, pG1), and
+        // each lane's (up to) two results: length | status << 24 and the literal's index in the fill
+        uint32_t pk = 0, pcur = 0, pG0 = 0, pG1 = 0;
+        uint32_t rv0 = 0, rv1 = 0, ri0 = 0xFFFFFFFFu, ri1 = 0xFFFFFFFFu;
+        uint32_t stop = 0;  // s_ctr[0] as read at the previous fill: another wave saw bad offsets
+        stamp(11);
+        // (LDS addresses of the per-fill transfers are made from an opaque copy of the lane index, so
+        // the compiler recomputes them where they are used instead of hoisting a register per round
+        // out of the fill loop: hoisted, they spilled, and every reload waited for all memory traffic)
+        auto opaque = [](uint32_t x) {
+            asm volatile("" : "+v"(x));
+            return x;
+        };
+        auto flush = [&]() {  // the previous fill's image span and results to global memory
+            const uint32_t ob = pG0 & ~15u;
+            const uint32_t c0 = ob >> 4, c1 = (pG1 + 15u) >> 4;
+            const uint4* l16 = reinterpret_cast<const uint4*>(s_img) + (opaque(lane) - lane);
+            uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
+            if (kMode != 2) {
+                // every LDS read first (one wait), then the stores
+                uint4 v[F];
+                bool w[F];
+#pragma unroll
+                for (int r = 0; r < F; ++r) {
+                    const uint32_t ci = c0 + lane + 64u * r;
+                    w[r] = ci < c1 && (ci << 4) >= pG0 && (ci << 4) + 16u <= pG1;
+                    v[r] = l16[min(ci - c0, (uint32_t)G::kImg / 16u - 1u)];
+                }
+                const uint32_t g = lane < 16 ? c0 << 4 : (c1 - 1u) << 4;  // the partial chunks at the two ends
+                const bool partial = lane < 32 && !(g >= pG0 && g + 16u <= pG1) && (lane < 16 || c1 - 1u != c0);
+                const uint32_t x = g + (lane & 15u);
+                const uint8_t pb = s_img[min(x - ob, (uint32_t)G::kImg - 1u)];
+#pragma unroll
+                for (int r = 0; r < F; ++r)
+                    if (w[r]) g16[c0 + lane + 64u * r] = v[r];
+                if (partial && x >= pG0 && x < pG1) a.out_base[x] = pb;
+            }
+            if (ri0 != 0xFFFFFFFFu) {
+                a.out_len[pcur + ri0] = rv0 & 0xFFFFFFu;
+                a.status[pcur + ri0] = (uint8_t)(rv0 >> 24);
+            }
+            if (ri1 != 0xFFFFFFFFu) {
+                a.out_len[pcur + ri1] = rv1 & 0xFFFFFFu;
+                a.status[pcur + ri1] = (uint8_t)(rv1 >> 24);
+            }
+            ri0 = ri1 = 0xFFFFFFFFu;
+        };
+        while (cur < ce) {  // wave-uniform
+            const uint32_t cntl = min(128u, ce - cur);
+            const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
+            // 1. offsets: bounds (bad), what fits
+            bool bad = false;
+            uint32_t ex[2], ey[2];
+            bool fits[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t t = lane + 64u * r;
+                bad |= t < cntl && !(io0[r] <= io1[r] && io1[r] <= a.in_cap && oo0[r] <= oo1[r] && oo1[r] <= a.out_cap);
+                const uint32_t p0 = io0[r] + a.in_mis, p1 = io1[r] + a.in_mis;
+                const uint32_t o0 = oo0[r] + a.out_mis, o1 = oo1[r] + a.out_mis;
+                fits[r] = t < cntl && p1 - base16 <= (uint32_t)kWinB && o1 - ob16 <= (uint32_t)G::kImg;
+                const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
+                const bool fast = ocap >= (nbytes * 8u) / 5u;
+                ex[r] = (p0 - base16) | (nbytes << 16);
+                ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
+            }
+            const bool wbad = __any(bad) || stop != 0u;
+            stamp(1);
+            if (kMode == 3) dg[8] += 1;
+            if (wbad) {  // the rest of the wave's chunks is void; nothing more is decoded or written here
+                if (pk) flush();
+                pk = 0;
+                if (lane == 0) {
+                    *a.err = 1u;
+                    s_ctr[0] = 1u;
+                }
+                for (;;) {  // this chunk's rest, the claimed next one, then every chunk still unclaimed
+                    for (uint32_t i = cur + lane; i < ce; i += 64u) {
+                        a.out_len[i] = 0;
+                        a.status[i] = (uint8_t)HPK_BAD_OFFSETS;
+                    }
+                    if (na >= ne) break;
+                    cur = na;
+                    ce = ne;
+                    claim(na, ne);
+                }
+                break;
+            }
+            // the fitting literals form a prefix (offsets are non-decreasing)
+            const uint64_t f0 = __ballot(fits[0]), f1 = __ballot(fits[1]);
+            const uint32_t k = (uint32_t)__popcll(f0) + (uint32_t)__popcll(f1);  // (wave-uniform)
+            if (k == 0) {  // literal `cur` alone exceeds the window or the image
+                if (pk) flush();
+                pk = 0;
+                const uint32_t nb = a.in_off[cur + 1] - a.in_off[cur];
+                const bool left = nb >= a.long_min && a.out_off[cur + 1] - a.out_off[cur] >= (nb * 8u) / 5u;
+                if (lane == 0) {
+                    if (left) {
+                        leave(cur, nb);
+                    } else {
+                        const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), last16 * 4 + 3};
+                        uint8_t* dst = a.out_base + gout;
+                        Lit L = {};
+                        lit_bytes_to(L, g, s_lo, [&](uint32_t j, uint8_t v) { dst[j] = v; },
+                                     a.out_off[cur + 1] - a.out_off[cur], gin, a.in_off[cur + 1] + a.in_mis - gin);
+                        a.out_len[cur] = L.cnt;
+                        a.status[cur] = (uint8_t)lit_status(L);
+                    }
+                }
+                cur += 1;
+                if (cur == ce) {  // the next chunk
+                    cur = na;
+                    ce = ne;
+                    claim(na, ne);
+                    if (na < ne) {
+                        ngin = a.in_off[na];
+                        ngout = a.out_off[na];
+                    }
+                }
+                if (cur < ce) {
+                    gin = a.in_off[cur] + a.in_mis;
+                    gout = a.out_off[cur] + a.out_mis;
+                    prefetch(cur, ce, gin & ~15u);
+                }
+                continue;
+            }
+            // the fill's end: the last fitting literal's offsets
+            const uint64_t fl = f1 ? f1 : f0;
+            const int hl = 63 - __builtin_clzll(fl);
+            const uint32_t gin_end = (uint32_t)__builtin_amdgcn_readlane((int)((f1 ? io1[1] : io1[0]) + a.in_mis), hl);
+            const uint32_t gout_end =
+                (uint32_t)__builtin_amdgcn_readlane((int)((f1 ? oo1[1] : oo1[0]) + a.out_mis), hl);
+            // where the next fill starts: right after this one, or at the next chunk
+            uint32_t cur_n = cur + k, ce_n = ce, gin_n = gin_end, gout_n = gout_end;
+            if (cur_n == ce) {
+                cur_n = na;
+                ce_n = ne;
+                gin_n = ngin + a.in_mis;
+                gout_n = ngout + a.out_mis;
+                claim(na, ne);
+                if (na < ne) {
+                    ngin = a.in_off[na];
+                    ngout = a.out_off[na];
+                }
+            }
+            // 2. the previous fill's write-back (its image is read out before this fill's queue lands there)
+            if (pk) flush();
+            stamp(2);
+            // 3. queue, longest first: a rank per literal from ballots over 16 length classes of 4 bytes
+            // (no LDS round trip), long literals listed for the long-literal phase instead
+            bool qd[2];
+            uint32_t key[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t nbytes = ex[r] >> 16;
+                const bool lng = nbytes >= a.long_min && !(ey[r] & kQ7Byte);
+                if (fits[r] && lng) leave(cur + lane + 64u * r, nbytes);
+                qd[r] = fits[r] && !lng;
+                key[r] = min(nbytes >> 2, 15u);
+            }
+            uint32_t rank0 = 0, rank1 = 0, kq = 0;
+#pragma unroll
+            for (int c = 15; c >= 0; --c) {
+                const bool h0 = qd[0] && key[0] == (uint32_t)c, h1 = qd[1] && key[1] == (uint32_t)c;
+                const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+                const uint32_t p0 = (uint32_t)__popcll(m0);
+                const uint32_t b0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+                const uint32_t b1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                rank0 = h0 ? kq + b0 : rank0;
+                rank1 = h1 ? kq + p0 + b1 : rank1;
+                kq += p0 + (uint32_t)__popcll(m1);
+            }
+            uint2* const q = reinterpret_cast<uint2*>(s_img);  // 128 entries, in the image
+            if (qd[0]) q[rank0] = make_uint2(ex[0], ey[0]);
+            if (qd[1]) q[rank1] = make_uint2(ex[1], ey[1]);
+            stamp(3);
+            // 4. the window, big-endian dwords: bit P of the stream is bit 31 - P % 32 of dword P / 32
+            {
+                uint4* l16 = reinterpret_cast<uint4*>(s_win) + (opaque(lane) - lane);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint4 c = ch[r];
+                    if (lane + 64u * r < (uint32_t)kWinB / 16u)
+                        l16[lane + 64u * r] = make_uint4(__builtin_bswap32(c.x), __builtin_bswap32(c.y),
+                                                         __builtin_bswap32(c.z), __builtin_bswap32(c.w));
+                }
+            }
+            stamp(4);
+            // 5. the snake's two queue entries per lane (read before the image is decoded over), and
+            // the workgroup's stop flag for the next fill
+            const uint32_t t1 = lane, t2 = 127u - lane;
+            const uint2 e1 = kq ? q[min(t1, kq - 1u)] : make_uint2(0u, 0u);
+            const uint2 e2 = kq ? q[min(t2, kq - 1u)] : make_uint2(0u, 0u);
+            stop = *reinterpret_cast<volatile uint32_t*>(&s_ctr[0]);
+            // 6. the next fill's offsets and window, in flight while this one decodes
+            if (cur_n < ce_n) prefetch(cur_n, ce_n, gin_n & ~15u);
+            // 7. lane walks: slots t1 then t2
+            Lit12 L, N;
+            auto load = [&](Lit12& T, const uint2 e, uint32_t tt) {
+                T.act = tt < kq && !(e.y & kQ7Byte);
+                T.idx = e.y & 0xFFFu;
+                const uint32_t nb = e.x >> 16;
+                const uint32_t o = (e.y >> 12) & 0x1FFFFu;
+                T.X = (e.x & 0xFFFFu) * 8u + 31u;
+                T.Eb = T.X + (T.act ? nb * 8u : 0u);
+                T.o = o;
+                T.o0 = o;
+                T.st = HPK_OK;
+                T.prog = false;
+                lit12_load(T, win32);
+            };
+            load(L, e1, t1);
+            load(N, e2, t2);
+            bool nv = t2 < kq;
+            uint32_t sX = 0, sO = 0, sSt = 0;
+            bool s1 = false;
+            stamp(5);
+            if (kMode != 1) {
+                for (;;) {
+                    if (kMode == 3) dg[9] += 1;
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) lit12_step<kStore>(L, win32, s_lut, s_lo, s_img, dmy);
+                    const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
+                    if (__any(fin)) {
+                        const bool sw = fin & nv;
+                        if (sw) {
+                            sX = L.X;
+                            sO = L.o;
+                            sSt = L.st;
+                            s1 = L.act;
+                            L = N;
+                            nv = false;
+                        }
+                        if (!__any(!fin | sw)) break;
+                    }
+                }
+            }
+            stamp(6);
+            // results: the first slot's from its saved end state, the second's from the walk
+            if (s1) {
+                const uint32_t Eb = (e1.x & 0xFFFFu) * 8u + 31u + (e1.x >> 16) * 8u;
+                const uint32_t st = sSt != HPK_OK ? sSt : residual_status(Eb - sX, win_at(win32, sX - 31u));
+                rv0 = (sO - ((e1.y >> 12) & 0x1FFFFu)) | (st << 24);
+                ri0 = e1.y & 0xFFFu;
+            }
+            if (L.act) {
+                rv1 = (L.o - L.o0) | (lit12_status(L) << 24);
+                ri1 = L.idx;
+            }
+            if (kMode == 1) {  // diagnostic: no decode
+                rv0 = 0;
+                ri0 = t1 < kq ? e1.y & 0xFFFu : 0xFFFFFFFFu;
+            }
+            // 8. a literal whose region is below the decoded bound: code by code, capacity-checked
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint2 e = r == 0 ? e1 : e2;
+                const uint32_t tt = r == 0 ? t1 : t2;
+                if (tt < kq && (e.y & kQ7Byte)) {
+                    const uint32_t i = e.y & 0xFFFu;
+                    const uint32_t o = (e.y >> 12) & 0x1FFFFu;
+                    Lit B = {};
+                    lit_bytes_to(B, LdsSwapSrc{win32}, s_lo, [&](uint32_t j, uint8_t v) { s_img[o + j] = v; },
+                                 a.out_off[cur + i + 1] - a.out_off[cur + i], e.x & 0xFFFFu, e.x >> 16);
+                    if (r == 0) {
+                        rv0 = B.cnt | (lit_status(B) << 24);
+                        ri0 = i;
+                    } else {
+                        rv1 = B.cnt | (lit_status(B) << 24);
+                        ri1 = i;
+                    }
+                }
+            }
+            stamp(7);
+            pk = k;
+            pcur = cur;
+            pG0 = gout;
+            pG1 = gout_end;
+            cur = cur_n;
+            ce = ce_n;
+            gin = gin_n;
+            gout = gout_n;
+        }
+        if (pk) flush();
+        stamp(2);
+    }
+    // ---- the literals left to the long-literal phase ----
+    __syncthreads();  // every wave's fills, list entries and stores are out
+    const uint32_t c1 = s_ctr[1], c2 = s_ctr[2];
+    if (c1 + c2) {
+        static_assert(G::kWaveOff % 16 == 0, "long-phase rings");
+        uint8_t* const area = smem + G::kWaveOff;
+        long_phase<512, 8, 32, 0, G::kBlock>(a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area),
+                                            area + 512 * 32 * 4,
+                                            reinterpret_cast<uint4*>(area + 512 * (32 * 4 + HPK_LONG_OS)), s_lut, s_lo);
+    }
+    stamp(10);
+    if (kMode == 3 && lane < 12) {
+        dg[0] = __builtin_amdgcn_s_memtime() - t_start;
+        unsigned long long v = 0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) v = lane == (uint32_t)i ? dg[i] : v;
+        a.dbg[((uint64_t)blockIdx.x * G::kWaves + wv) * 16u + lane] = v;
+    }
+}
+
+}  // namespace hpkdec

@@ -54,6 +54,17 @@ def _wire(t):
     return t
 
 
+def _check(t, name, kinds):
+    """Refuse, before any message is posted, a tensor the receiving side would misread: the receiver
+    allocates int32 / uint8 buffers from the sizes alone, so an int64 offset tensor or a strided view
+    would be a size mismatch on the wire (an RCCL hang, or garbage), not an error."""
+    dt = str(t.dtype).replace("torch.", "")
+    if dt not in kinds:
+        raise ValueError(f"{name}: dtype {dt} not in {kinds}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+
+
 def _p2p(dist, ops, group):
     if not ops:
         return
@@ -67,20 +78,61 @@ def owner(s: int, world: int) -> int:
     return s % world
 
 
+def compact_offsets(out_len, m):
+    """int64 offsets [m + 1] of m literals' decoded bytes laid end to end (exclusive sum of out_len)."""
+    import torch
+
+    off = torch.zeros(m + 1, dtype=torch.int64, device=out_len.device)
+    if m:
+        torch.cumsum(out_len[:m].to(torch.int64), 0, out=off[1:])
+    return off
+
+
+def compact(out_blob, out_off, out_len, m, total, chunk=1 << 28):
+    """The decoded bytes of m literals (literal i at out_off[i], out_len[i] bytes: the region layout a
+    decode writes) laid end to end: a uint8 tensor of `total` bytes on the same device (no host sync:
+    total is known). Built in pieces of ~`chunk` bytes so the index tensor stays bounded."""
+    import torch
+
+    dev = out_blob.device
+    res = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    if total == 0:
+        return res[:0]
+    ln = out_len[:m].to(torch.int64)
+    src = out_off[:m].to(torch.int64) & 0xFFFFFFFF
+    coff = compact_offsets(out_len, m)
+    # literal ranges of about `chunk` output bytes each (a host read of the cut points: one per piece)
+    cuts = torch.searchsorted(coff, torch.arange(0, total + chunk, chunk, device=dev, dtype=torch.int64)).tolist()
+    cuts = sorted(set([0] + [min(c, m) for c in cuts] + [m]))
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if a == b:
+            continue
+        x0, x1 = int(coff[a].item()), int(coff[b].item())
+        if x1 == x0:
+            continue
+        idx = torch.repeat_interleave(src[a:b] - (coff[a:b] - x0), ln[a:b], output_size=x1 - x0)
+        idx += torch.arange(x1 - x0, device=dev, dtype=torch.int64)
+        res[x0:x1] = out_blob[idx]
+    return res
+
+
 def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
     """Root-resident batch -> per-rank shards -> decode_fn on every rank -> results on root.
 
     shards (root only; ignored elsewhere): a list of (blob uint8, off int32/uint32 [m+1]) tensors
     on `device` — a batch already cut into shards of at most 4 GiB each (u32 offsets), e.g. by
     `balanced_ranges`. Shard s is decoded on rank owner(s, world); root keeps its own.
-    decode_fn(blob, off) -> (out_blob, out_off, out_len, status) tensors on `device`.
+    decode_fn(blob, off) -> (out_blob, out_off, out_len int32/uint32, status uint8) on `device`.
 
-    Everything stays in device memory when `device` is a GPU (RCCL point-to-point over xGMI: one
-    grouped send/recv round out, one back; no host copy): the shard sizes go out with one broadcast,
-    the offsets and blob of each shard with one grouped send/recv, the decoded blob, out_off,
-    out_len and status come back the same way. With gloo and CPU tensors the same code runs on the
-    host (tests/test_shard.py). Returns on root the list of (out_blob, out_off, out_len, status)
-    in shard order; None elsewhere."""
+    Everything stays in device memory when `device` is a GPU (RCCL point-to-point over xGMI; no host
+    copy of the data): the shard sizes go out with one broadcast and the offsets and blob of each
+    shard with one grouped send/recv round. Every owner then lays its shards' decoded bytes end to
+    end (only out_len bytes per literal travel back, not the regions' slack), one all-reduce tells
+    root every shard's decoded size, and the bytes, out_len and status come back in one more grouped
+    round. Host synchronisation: the size broadcast and the all-reduce, once each, whatever the
+    number of shards. With gloo and CPU tensors the same code runs on the host (tests/test_shard.py).
+    Returns on root the list of (decoded bytes laid end to end, their int64 offsets [m+1], out_len,
+    status) in shard order; None elsewhere."""
     import torch
     import torch.distributed as dist
 
@@ -91,6 +143,9 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
     dist.broadcast(cnt, root, group=group)
     S = int(cnt.item())
     if rank == root:
+        for s, (b, off) in enumerate(shards):
+            _check(off, f"shard {s} offsets", ("int32", "uint32"))
+            _check(b, f"shard {s} blob", ("uint8",))
         meta = torch.tensor([[int(o.numel()) - 1, int(b.numel())] for b, o in shards], dtype=torch.int64,
                             device=dev).reshape(S, 2)
     else:
@@ -119,51 +174,51 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
         elif rank == root:
             local[s] = shards[s]
     _p2p(dist, ops, group)
-    # 3. decode the local shards
+    # 3. decode the local shards; every shard's decoded size, on the device
     res = {s: decode_fn(*local[s]) for s in mine}
-    # 4. gather: output sizes first, then out_off, out_len, status and the decoded blob
-    hdr, ops = {}, []
-    for s in range(S):
-        o = owner(s, world)
-        if o == root:
-            continue
-        if rank == o:
-            ob = res[s][1]
-            hdr[s] = torch.tensor([int(ob[-1].item()) & 0xFFFFFFFF], dtype=torch.int64, device=dev)
-            ops.append((dist.isend, hdr[s], root))
-        elif rank == root:
-            hdr[s] = torch.empty(1, dtype=torch.int64, device=dev)
-            ops.append((dist.irecv, hdr[s], o))
-    _p2p(dist, ops, group)
+    tot = torch.zeros(max(S, 1), dtype=torch.int64, device=dev)
+    for s in mine:
+        ob, oo, ol, st = res[s]
+        _check(ol, f"shard {s} out_len", ("int32", "uint32"))
+        _check(st, f"shard {s} status", ("uint8",))
+        m = sizes[s][0]
+        if m:
+            tot[s] = ol[:m].to(torch.int64).sum()
+    # 4. one all-reduce: every rank (root included) learns every shard's decoded size
+    if S:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+    totals = tot.tolist()
+    # 5. the owners lay their shards' bytes end to end; bytes, out_len and status go to root
+    packed = {s: compact(*res[s][:3], sizes[s][0], int(totals[s])) for s in mine}
     out, ops = {}, []
     for s in range(S):
         o = owner(s, world)
-        m = sizes[s][0]
+        m, nbytes = sizes[s][0], int(totals[s])
         if o == root:
             continue
         if rank == o:
-            ob, oo, ol, st = res[s]
-            nbytes = int(hdr[s].item())
-            ops += [(dist.isend, _wire(oo[: m + 1]), root), (dist.isend, _wire(ol[:m]), root),
-                    (dist.isend, st[:m], root)]
+            ol, st = res[s][2], res[s][3]
+            ops += [(dist.isend, _wire(ol[:m]), root), (dist.isend, st[:m], root)]
             if nbytes:
-                ops.append((dist.isend, ob[:nbytes], root))
+                ops.append((dist.isend, packed[s], root))
         elif rank == root:
-            nbytes = int(hdr[s].item())
-            oo = torch.empty(m + 1, dtype=torch.int32, device=dev)
             ol = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
             st = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
-            ob = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-            ops += [(dist.irecv, oo, o), (dist.irecv, ol[:m], o), (dist.irecv, st[:m], o)]
+            cb = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+            ops += [(dist.irecv, ol[:m], o), (dist.irecv, st[:m], o)]
             if nbytes:
-                ops.append((dist.irecv, ob[:nbytes], o))
-            out[s] = (ob, oo, ol[:m], st[:m])
+                ops.append((dist.irecv, cb[:nbytes], o))
+            out[s] = (cb[:nbytes], ol[:m], st[:m])
     ops = [x for x in ops if x[1].numel()]
     _p2p(dist, ops, group)
     if rank != root:
         return None
-    for s in mine:
-        ob, oo, ol, st = res[s]
+    result = []
+    for s in range(S):
         m = sizes[s][0]
-        out[s] = (ob, oo, ol[:m], st[:m])
-    return [out[s] for s in range(S)]
+        if s in mine:
+            cb, ol, st = packed[s], res[s][2][:m], res[s][3][:m]
+        else:
+            cb, ol, st = out[s]
+        result.append((cb, compact_offsets(ol, m), ol, st))
+    return result

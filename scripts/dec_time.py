@@ -53,7 +53,8 @@ def main():
                       "checked": os.environ.get("HPK_DEBUG_MODE", "0") in ("0", "3", "4", "5"),
                       "long_min": os.environ.get("HPK_LONG_MIN", "default"),
                       "lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")),
-                      "debug_mode": os.environ.get("HPK_DEBUG_MODE", "0")}), flush=True)
+                      "debug_mode": os.environ.get("HPK_DEBUG_MODE", "0"),
+                      "kernel": os.environ.get("HPK_DECODE_KERNEL", "auto")}), flush=True)
 
 
 if __name__ == "__main__":

@@ -15,13 +15,16 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module")
-def codec():
+@pytest.fixture(scope="module", params=["fill", "wave"])
+def codec(request):
+    """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the v24
+    workgroup fills and the v25 wave fills), which must give identical results."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a GPU (run with -m 'not gpu' on CPU)")
     from loona_amd import HuffmanCodec
 
     c = HuffmanCodec(0, stream=torch.cuda.current_stream())
+    c.set_decode_kernel(request.param)
     yield c
     c.close()
 
@@ -136,12 +139,13 @@ def test_long_literals(codec):
 
 
 def test_split_long_literals(codec):
-    """v22: literals of 1.5-6 KiB encoded (left to the long-literal phase) are decoded as two pieces by
-    two lanes and joined where their walks meet. Text and random bytes (long codes: the pieces meet
-    late), an EOS before, near and after the split byte at every offset class mod 64 bits, bad and
-    too-long padding, a run of ones from the middle on (the second piece starts in an EOS), literals
-    just below and above the split range, at exact-bound regions on an unaligned base with guard
-    bytes. Bit-exact (lengths, statuses, bytes) against the oracle."""
+    """Literals of 1.5-6 KiB encoded (left to the long-literal phase, one lane each, hpk_long.h):
+    text and random bytes (long codes), an EOS before, near and after the middle byte at every
+    offset class mod 64 bits, bad and too-long padding, a run of ones from the middle on, literals
+    just below and above that size range, at exact-bound regions on an unaligned base with guard
+    bytes. Bit-exact (lengths, statuses, bytes) against the oracle. (Written for the v22 experiment
+    that split such literals into two pieces joined where their walks met; that split measured
+    slower and was reverted, the cases stay as long-literal coverage.)"""
     from loona_amd import huffman_encode
 
     rng = np.random.default_rng(2207)
@@ -627,7 +631,9 @@ def test_bad_offsets_with_long_literals_in_the_fill(codec):
                           to_dev(oo.astype(np.uint32).view(np.int32)), ol, st, device=True, sync=True)
     stn, oln = st.cpu().numpy(), ol.cpu().numpy()
     bad = stn == _lib.HPK_BAD_OFFSETS
-    assert bad[j : j + 7].all(), stn[j : j + 7]  # the long literals after j in its fill included
+    # the long literal after j in its fill included (j + 1 shares j's fill under both kernels: the
+    # workgroup kernel voids its whole range from the bad fill on, the wave kernel its wave's range)
+    assert bad[j : j + 2].all(), stn[j : j + 7]
     assert (oln[bad] == 0).all()
     assert set(np.unique(stn)) <= {0, _lib.HPK_BAD_OFFSETS}
     good_long = [i for i in range(0, n, 997) if not bad[i]]
@@ -783,11 +789,11 @@ def test_scatter_decode_gather_device_world1(codec):
 
         res = shard.scatter_decode_gather(shards, decode_fn, device="cuda")
         torch.cuda.synchronize()
-        for r, (ob, oo, ol, st) in enumerate(res):
+        for r, (cb, coff, ol, st) in enumerate(res):  # each shard's decoded bytes laid end to end
             lo, hi = int(b[r]), int(b[r + 1])
             sb, so = shard.shard(w.enc_blob, w.enc_off, lo, hi)
-            got = (ob.cpu().numpy(), oo.cpu().numpy().view(np.uint32), ol.cpu().numpy().view(np.uint32)[: hi - lo],
-                   st.cpu().numpy()[: hi - lo])
+            cbh = cb.cpu().numpy() if cb.numel() else np.zeros(1, np.uint8)
+            got = (cbh, coff.cpu().numpy().astype(np.uint32), ol.cpu().numpy().view(np.uint32), st.cpu().numpy())
             compare_batches(got, oracle_decode_batch(sb, so), f"world-1 shard {r}")
     finally:
         dist.destroy_process_group()

@@ -37,6 +37,24 @@ def test_balanced_ranges_cover_and_balance():
             assert p[1][0] == 0 and int(p[1][-1]) == len(p[0])
 
 
+def test_compact_and_wire_checks():
+    """compact() lays a region-layout decode end to end; scatter_decode_gather refuses offsets the
+    receiver would misread (int64, views) before posting anything."""
+    import torch
+
+    blob, off = _lits(3000, 4)
+    ob, oo, ol, st = decode_batch_cpu(blob, off, nthreads=2)
+    m = len(off) - 1
+    cb = shard.compact(torch.from_numpy(ob), torch.from_numpy(oo.view(np.int32)), torch.from_numpy(ol.view(np.int32)),
+                       m, int(ol.astype(np.int64).sum()), chunk=4096)
+    want = b"".join(ob[oo[i] : oo[i] + ol[i]].tobytes() for i in range(m))
+    assert cb.numpy().tobytes() == want
+    with pytest.raises(ValueError, match="dtype"):
+        shard._check(torch.zeros(4, dtype=torch.int64), "off", ("int32", "uint32"))
+    with pytest.raises(ValueError, match="contiguous"):
+        shard._check(torch.zeros(8, dtype=torch.int32)[::2], "off", ("int32", "uint32"))
+
+
 def test_balanced_ranges_edge_cases():
     assert list(shard.balanced_ranges(np.zeros(1, np.uint32), 4)) == [0, 0, 0, 0, 0]
     off = np.array([0, 0, 0, 5], np.uint32)  # empty literals then one
@@ -107,13 +125,14 @@ def test_scatter_decode_gather_gloo(world, nshards):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert len(res) == nshards
-    # concatenate the shards' results with rebased output offsets
-    out_blob = np.concatenate([r[0][: int(r[1].view(np.uint32)[-1])] for r in res])
+    # each shard comes back laid end to end (int64 offsets = exclusive sum of out_len): concatenate
+    for cb, coff, ol, st in res:
+        assert coff[0] == 0 and int(coff[-1]) == cb.size and np.array_equal(np.diff(coff), ol.astype(np.int64))
+    out_blob = np.concatenate([r[0] for r in res])
     offs, base = [np.zeros(1, np.int64)], 0
     for r in res:
-        oo = r[1].view(np.uint32).astype(np.int64)
-        offs.append(oo[1:] + base)
-        base += int(oo[-1])
+        offs.append(r[1][1:] + base)
+        base += int(r[1][-1])
     got = (out_blob, np.concatenate(offs).astype(np.uint32), np.concatenate([r[2].view(np.uint32) for r in res]),
            np.concatenate([r[3] for r in res]))
     blob, off = _lits(n, seed)
