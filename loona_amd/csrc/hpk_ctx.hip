@@ -123,6 +123,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
+    if (c->h_pin) (void)hipHostFree(c->h_pin);
     for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
         if (c->long_ev_set[j]) (void)hipEventSynchronize(c->long_ev[j]);
         if (c->long_list[j]) (void)hipFree(c->long_list[j]);
@@ -156,6 +157,25 @@ extern "C" int hpk_host_register(void* ptr, size_t bytes) {
 extern "C" int hpk_host_unregister(void* ptr) {
     if (!ptr) return hpk_set_err_msg("null pointer", HPK_E_INVAL);
     HIP_TRY(hipHostUnregister(ptr));
+    return HPK_E_OK;
+}
+
+// The context's page-locked host staging area (grow-only): the block-level calls build their
+// Huffman batch in it so the batch's copies DMA straight from it. Growing waits for the context's
+// stream (the old area may still be the source or target of its copies).
+int hpk_ctx_pinned(hpk_ctx* c, size_t bytes, void** p) {
+    if (bytes > c->h_pin_cap) {
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->d2h) HIP_TRY(hipStreamSynchronize(c->d2h));
+        if (c->h_pin) (void)hipHostFree(c->h_pin);
+        c->h_pin = nullptr;
+        c->h_pin_cap = 0;
+        const size_t cap = bytes + bytes / 4 + (1u << 20);
+        HIP_TRY(hipHostMalloc(&c->h_pin, cap, hipHostMallocDefault));
+        c->h_pin_cap = cap;
+    }
+    *p = c->h_pin;
     return HPK_E_OK;
 }
 

@@ -29,6 +29,9 @@ struct hpk_ctx {
     size_t d_meta_cap = 0;
     uint8_t* d_st = nullptr;
     size_t d_st_cap = 0;
+    // page-locked host staging for the block-level calls (hpk_ctx_pinned), grow-only
+    void* h_pin = nullptr;
+    size_t h_pin_cap = 0;
     // host-pointer pipeline: copy-in and copy-out streams + per-chunk events (created lazily)
     static constexpr int kMaxChunks = 8;
     hipStream_t h2d = nullptr;

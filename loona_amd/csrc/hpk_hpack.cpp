@@ -27,6 +27,8 @@
 #include "../../include/hpk.h"
 
 int hpk_set_err_msg(const char* what, int code);  // hpk_ctx.hip: hpk_last_error's message
+// hpk_ctx.hip: the context's page-locked host staging area, grown to at least `bytes` (grow-only)
+int hpk_ctx_pinned(hpk_ctx* ctx, size_t bytes, void** p);
 
 namespace {
 
@@ -311,11 +313,11 @@ uint32_t put(Out& o, const void* p, size_t n) {
     return at;
 }
 
-struct Huff {
-    const std::vector<uint8_t>* out;
-    const std::vector<uint32_t>* oo;
-    const std::vector<uint32_t>* len;
-    const std::vector<uint8_t>* st;
+struct Huff {  // the Huffman batch's results (host memory: pageable vectors or the ctx's pinned area)
+    const uint8_t* out;
+    const uint32_t* oo;
+    const uint32_t* len;
+    const uint8_t* st;
 };
 
 // Pass 3 for one block: the reference's single pass over the scanned fields.
@@ -333,14 +335,14 @@ void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const std::ve
     // string bytes: raw from the block, Huffman from the batch (status checked by the caller)
     auto str = [&](const Str& s, const uint8_t** p, size_t* n) {
         if (s.huff) {
-            *p = h.out->data() + (*h.oo)[s.lit];
-            *n = (*h.len)[s.lit];
+            *p = h.out + h.oo[s.lit];
+            *n = h.len[s.lit];
         } else {
             *p = base + s.off;
             *n = s.len;
         }
     };
-    auto huff_err = [&](const Str& s) -> int { return s.huff ? (*h.st)[s.lit] : 0; };
+    auto huff_err = [&](const Str& s) -> int { return s.huff ? h.st[s.lit] : 0; };
     bool last_was_size_update = false;
     for (size_t fi = 0; fi < sc.n; ++fi) {
         const Field& f = fields[fi];
@@ -487,15 +489,46 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
     });
     const long us_scan = us(t_0);
     auto t_1 = now();
-    // pass 2: one batch for all of them
+    // pass 2: one batch for all of them. With a device context the batch is staged in the context's
+    // page-locked host area (hpk_ctx_pinned), so its copies are DMA transfers that overlap the kernel
+    // chunk by chunk; pageable vectors made HIP bounce every byte through its own staging buffer.
     const uint32_t n = lbase[nth];
-    std::vector<uint32_t>&in_off = W.in_off, &out_off = W.out_off, &len = W.len;
-    std::vector<uint8_t>& st = W.st;
-    in_off.resize(n + 1);
-    out_off.resize(n + 1);
-    len.resize(n ? n : 1);
-    st.resize(n ? n : 1);
     size_t tot = 0, otot = 0;
+    for (int t = 0; t < nth; ++t)
+        for (size_t j = 0; j < thlen[t].size(); ++j) {
+            tot += thlen[t][j];
+            otot += ((hpk_decoded_bound(thlen[t][j]) + 3) & ~(size_t)3);
+            if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
+        }
+    uint8_t *in, *dec, *st;
+    uint32_t *in_off, *out_off, *len;
+    const size_t in_b = (tot + 16 + 15) & ~(size_t)15, dec_b = (otot + 16 + 15) & ~(size_t)15;
+    const size_t off_b = ((size_t)(n + 1) * 4 + 15) & ~(size_t)15;
+    if (ctx) {
+        uint8_t* base = nullptr;
+        if (int rc = hpk_ctx_pinned(ctx, in_b + dec_b + 3 * off_b + n + 16, (void**)&base)) return rc;
+        in = base;
+        dec = in + in_b;
+        in_off = (uint32_t*)(dec + dec_b);
+        out_off = (uint32_t*)((uint8_t*)in_off + off_b);
+        len = (uint32_t*)((uint8_t*)out_off + off_b);
+        st = (uint8_t*)len + off_b;
+    } else {
+        W.in.resize(in_b);
+        W.dec.resize(dec_b);
+        W.in_off.resize(n + 1);
+        W.out_off.resize(n + 1);
+        W.len.resize(n ? n : 1);
+        W.st.resize(n ? n : 1);
+        in = W.in.data();
+        dec = W.dec.data();
+        in_off = W.in_off.data();
+        out_off = W.out_off.data();
+        len = W.len.data();
+        st = W.st.data();
+    }
+    tot = 0;
+    otot = 0;
     for (int t = 0; t < nth; ++t)
         for (size_t j = 0; j < thlen[t].size(); ++j) {
             const uint32_t i = lbase[t] + (uint32_t)j;
@@ -503,22 +536,16 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
             out_off[i] = (uint32_t)otot;
             tot += thlen[t][j];
             otot += ((hpk_decoded_bound(thlen[t][j]) + 3) & ~(size_t)3);
-            if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
         }
     in_off[n] = (uint32_t)tot;
     out_off[n] = (uint32_t)otot;
-    std::vector<uint8_t>&in = W.in, &dec = W.dec;
-    in.resize(tot ? tot : 1);
-    dec.resize(otot ? otot : 1);
     parallel([&](int t) {
         for (size_t j = 0; j < thoff[t].size(); ++j)
-            memcpy(in.data() + in_off[lbase[t] + j], blocks + thoff[t][j], thlen[t][j]);
+            memcpy(in + in_off[lbase[t] + j], blocks + thoff[t][j], thlen[t][j]);
     });
     if (n) {
-        const int rc = ctx ? hpk_decode_batch(ctx, in.data(), in.size(), in_off.data(), n, dec.data(), dec.size(), out_off.data(),
-                                              len.data(), st.data(), HPK_PTR_HOST)
-                           : hpk_decode_batch_cpu(in.data(), in_off.data(), n, dec.data(), out_off.data(), len.data(),
-                                                  st.data(), 0);
+        const int rc = ctx ? hpk_decode_batch(ctx, in, in_b, in_off, n, dec, dec_b, out_off, len, st, HPK_PTR_HOST)
+                           : hpk_decode_batch_cpu(in, in_off, n, dec, out_off, len, st, 0);
         if (rc) return rc;
     }
     const long us_batch = us(t_1);
@@ -540,7 +567,7 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
     owner.resize(nblocks);
     for (uint32_t b = 0; b < nblocks; ++b)
         owner[b] = (uint8_t)(((uintptr_t)decs[b] >> 4) * 0x9E3779B97F4A7C15ull >> 59) % (uint32_t)nth;
-    const Huff h{&dec, &out_off, &len, &st};
+    const Huff h{dec, out_off, len, st};
     parallel([&](int t) {
         Out mine = std::move(outs[t]);  // (a local: no false sharing with the neighbours' headers)
         for (uint32_t b = 0; b < nblocks; ++b)

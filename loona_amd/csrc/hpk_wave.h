@@ -36,6 +36,74 @@
 
 namespace hpkdec {
 
+// Append g (<= 5) decoded bytes p (little-endian, zero above them) to a lane's pending output (acc,
+// accn <= 3 bytes) and store the dword once it is full: out32[o] (o a dword index), else the lane's
+// dummy dword, so the store is unconditional (no exec-mask branch).
+__device__ __forceinline__ void dw_append(uint32_t& o, uint32_t& acc, uint32_t& accn, uint32_t* __restrict__ out32,
+                                          uint32_t dmy32, uint32_t p, uint32_t g) {
+    const uint64_t x = (uint64_t)p << (8u * accn);
+    const uint32_t lo = acc | (uint32_t)x;
+    const uint32_t n2 = accn + g;
+    const bool full = n2 >= 4u;
+    out32[full ? o : dmy32] = lo;
+    o += full ? 1u : 0u;
+    acc = full ? (uint32_t)(x >> 32) : lo;
+    accn = n2 & 3u;
+}
+
+// lit12_step with dword output (v25b): the step's (up to four) bytes are gathered with v_perm and
+// appended to the lane's pending dword, ONE LDS store per step instead of four byte stores (a
+// literal's region must start and end on a dword). L.o counts dwords; acc / accn are the pending
+// bytes.
+__device__ __forceinline__ void lit12_step_dw(Lit12& L, uint32_t& acc, uint32_t& accn,
+                                              const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                              const uint16_t* __restrict__ lo, uint32_t* __restrict__ out32,
+                                              uint32_t dmy32) {
+    const uint32_t d3 = win32[(L.X >> 5) + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t rem = L.Eb - L.X;
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+    bool a1, a2;
+    const uint32_t u1 = lut12(e1, rem, a1, a2);
+    bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
+    const bool cont = a1 & (a2 | (e1 >= HPK_LUT2_NOTTWO));
+    const uint32_t w2 = w << u1;
+    const uint32_t rem2 = rem - u1;
+    const uint32_t e2 = lut[w2 >> (32 - HPK_LUT_BITS)];
+    bool b1, b2;
+    const uint32_t u2 = lut12(e2, rem2, b1, b2);
+    park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
+    b1 &= cont;
+    b2 &= cont;
+    const uint32_t g1 = (uint32_t)a1 + (uint32_t)a2, g2 = (uint32_t)b1 + (uint32_t)b2;
+    dw_append(L.o, acc, accn, out32, dmy32, lut12_bytes(e1, g1) | (lut12_bytes(e2, g2) << (8u * g1)), g1 + g2);
+    const uint32_t xn = L.X + u1 + (cont ? u2 : 0u);
+    const bool cross = (xn ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xn;
+    L.prog = a1 | park;
+    if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
+        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+        uint32_t sy, len;
+        bool eos;
+        lo_decode(wp, lo, sy, len, eos);
+        const uint32_t r = L.Eb - L.X;
+        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+            L.st = HPK_PADDING_TOO_LARGE;
+            L.Eb = L.X;
+        } else if (eos) {  // huffman.rs:112-116
+            L.st = HPK_EOS_IN_STRING;
+            L.Eb = L.X;
+        } else {
+            dw_append(L.o, acc, accn, out32, dmy32, sy, 1u);
+            L.X += len;
+            lit12_load(L, win32);
+        }
+    }
+}
+
 template <int kWinB, int kImgB>
 struct GeoW {
     static constexpr int kWaves = 16, kBlock = kWaves * 64;
@@ -56,7 +124,9 @@ struct GeoW {
 // WG counters (s_ctr): [0] bad offsets seen (waves stop at their next fill), [1] long list, front
 // (>= long_big bytes), [2] long list, back, [3] long-phase claim, [4]/[5] dense check sums, [6] the
 // dense listing found an entry it cannot list, [7] chunks of kChunk literals handed out to the waves
-template <int kMode, int kWinB, int kImgB, uint32_t kChunk>
+// kRank: 0 = counting sort with LDS atomics on 32 length classes of 2 bytes, 1 / 2 = ranks from
+// ballots over 16 classes of 4 bytes / 32 classes of 2 bytes (no LDS round trip)
+template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kDw, bool kGuided, int kRank>
 __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     using G = GeoW<kWinB, kImgB>;
     constexpr int kStore = kMode == 2 ? kNoStore : kPred;
@@ -146,18 +216,33 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         uint8_t* const s_img = s_win + kWinB;
         const uint32_t* const win32 = reinterpret_cast<const uint32_t*>(s_win);
         const uint32_t dmy = (uint32_t)G::kImg + lane * 4u;
-        // The workgroup's range is handed out in chunks of kChunk literals (about two fills), in order,
-        // to whichever wave asks next (an LDS counter): a static split left the waves the SIMDs'
-        // arbitration favours idle at the end while the others finished (11 % of a wave's time).
-        // A wave holds its current chunk and has already claimed the next one, whose first offsets are
-        // loaded a fill ahead of their use.
+        // The workgroup's range is handed out in chunks, in order, to whichever wave asks next (an LDS
+        // cursor): a static split left the waves the SIMDs' arbitration favours idle at the end while
+        // the others finished (11 % of a wave's time). Chunks shrink as the range drains (guided
+        // self-scheduling: 1/32 of what is left, at least kChunk literals), so early chunks hold many
+        // fills (a chunk's last fill is usually partial) and the last ones even the waves out. A wave
+        // holds its current chunk and has already claimed the next one, whose first offsets are loaded a
+        // fill ahead of their use.
+        // (!kGuided: the wave's static 1/16 of the range, then nothing)
+        bool given = false;
         auto claim = [&](uint32_t& ca, uint32_t& ce) {
+            if (!kGuided) {
+                ca = given ? BB : BA + (uint32_t)((uint64_t)(BB - BA) * wv / G::kWaves);
+                ce = given ? BB : BA + (uint32_t)((uint64_t)(BB - BA) * (wv + 1) / G::kWaves);
+                given = true;
+                return;
+            }
             uint32_t c = 0;
-            if (lane == 0) c = atomicAdd(&s_ctr[7], 1u);
-            c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-            const uint64_t lo = (uint64_t)BA + (uint64_t)c * kChunk;
-            ca = (uint32_t)min(lo, (uint64_t)BB);
-            ce = (uint32_t)min(lo + kChunk, (uint64_t)BB);
+            if (lane == 0) {
+                const uint32_t seen = *reinterpret_cast<volatile uint32_t*>(&s_ctr[7]);
+                const uint32_t left = BB - BA > seen ? BB - BA - seen : 0u;
+                const uint32_t want = max(kChunk, left / 32u);
+                c = atomicAdd(&s_ctr[7], want);
+                c = c < BB - BA ? c : BB - BA;
+                ce = BA + min(c + want, BB - BA);  // (lane 0's; broadcast below)
+            }
+            ca = BA + (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+            ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)ce);
         };
         // registers of the next fill: offsets of slots lane and lane + 64, the window chunks
         uint32_t io0[2], io1[2], oo0[2], oo1[2];
@@ -208,23 +293,17 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             const uint4* l16 = reinterpret_cast<const uint4*>(s_img) + (opaque(lane) - lane);
             uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
             if (kMode != 2) {
-                // every LDS read first (one wait), then the stores
-                uint4 v[F];
-                bool w[F];
 #pragma unroll
                 for (int r = 0; r < F; ++r) {
                     const uint32_t ci = c0 + lane + 64u * r;
-                    w[r] = ci < c1 && (ci << 4) >= pG0 && (ci << 4) + 16u <= pG1;
-                    v[r] = l16[min(ci - c0, (uint32_t)G::kImg / 16u - 1u)];
+                    if (ci < c1 && (ci << 4) >= pG0 && (ci << 4) + 16u <= pG1) g16[ci] = l16[ci - c0];
                 }
-                const uint32_t g = lane < 16 ? c0 << 4 : (c1 - 1u) << 4;  // the partial chunks at the two ends
-                const bool partial = lane < 32 && !(g >= pG0 && g + 16u <= pG1) && (lane < 16 || c1 - 1u != c0);
-                const uint32_t x = g + (lane & 15u);
-                const uint8_t pb = s_img[min(x - ob, (uint32_t)G::kImg - 1u)];
-#pragma unroll
-                for (int r = 0; r < F; ++r)
-                    if (w[r]) g16[c0 + lane + 64u * r] = v[r];
-                if (partial && x >= pG0 && x < pG1) a.out_base[x] = pb;
+                if (lane < 32) {  // the partial chunks at the two ends, one byte per lane
+                    const uint32_t g = lane < 16 ? c0 << 4 : (c1 - 1u) << 4;
+                    const bool partial = !(g >= pG0 && g + 16u <= pG1) && (lane < 16 || c1 - 1u != c0);
+                    const uint32_t x = g + (lane & 15u);
+                    if (partial && x >= pG0 && x < pG1) a.out_base[x] = s_img[x - ob];
+                }
             }
             if (ri0 != 0xFFFFFFFFu) {
                 a.out_len[pcur + ri0] = rv0 & 0xFFFFFFu;
@@ -242,7 +321,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             // 1. offsets: bounds (bad), what fits
             bool bad = false;
             uint32_t ex[2], ey[2];
-            bool fits[2];
+            bool fits[2], unal[2];  // unal: a region that does not start and end on a dword
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = lane + 64u * r;
@@ -254,6 +333,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const bool fast = ocap >= (nbytes * 8u) / 5u;
                 ex[r] = (p0 - base16) | (nbytes << 16);
                 ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
+                unal[r] = fast && ((o0 | ocap) & 3u) != 0u;
             }
             const bool wbad = __any(bad) || stop != 0u;
             stamp(1);
@@ -347,11 +427,34 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const bool lng = nbytes >= a.long_min && !(ey[r] & kQ7Byte);
                 if (fits[r] && lng) leave(cur + lane + 64u * r, nbytes);
                 qd[r] = fits[r] && !lng;
-                key[r] = min(nbytes >> 2, 15u);
+                key[r] = kRank == 1 ? min(nbytes >> 2, 15u) : min(nbytes >> 1, 31u);
             }
+            // dword output for this fill when every queued literal's region starts and ends on a dword
+            const bool dw = kDw && kStore == kPred && !__any((qd[0] && unal[0]) || (qd[1] && unal[1]));
             uint32_t rank0 = 0, rank1 = 0, kq = 0;
+            uint2* const q = reinterpret_cast<uint2*>(s_img + 256);  // 128 entries, in the image
+            if (kRank == 0) {  // counting sort: class counts by LDS atomics, bases by a wave scan
+                uint32_t* const hist = reinterpret_cast<uint32_t*>(s_img);  // 32 counts, then 32 bases
+                if (lane < 32) hist[lane] = 0;
+                const uint32_t pa = qd[0] ? atomicAdd(&hist[31u - key[0]], 1u) : 0u;
+                const uint32_t pb = qd[1] ? atomicAdd(&hist[31u - key[1]], 1u) : 0u;
+                const uint32_t v = lane < 32 ? hist[lane] : 0u;
+                // inclusive scan within rows of 16 lanes by DPP row shifts (no bpermute addresses to
+                // keep: as shuffles they were hoisted and spilled), then row 1 adds row 0's total
+                uint32_t x = v;
+                x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+                x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+                x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+                x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+                const uint32_t row0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+                x += lane >= 16u ? row0 : 0u;
+                if (lane < 32) hist[32 + lane] = x - v;
+                kq = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+                rank0 = qd[0] ? hist[32 + 31 - key[0]] + pa : 0u;
+                rank1 = qd[1] ? hist[32 + 31 - key[1]] + pb : 0u;
+            }
 #pragma unroll
-            for (int c = 15; c >= 0; --c) {
+            for (int c = (kRank == 1 ? 15 : 31); kRank != 0 && c >= 0; --c) {
                 const bool h0 = qd[0] && key[0] == (uint32_t)c, h1 = qd[1] && key[1] == (uint32_t)c;
                 const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
                 const uint32_t p0 = (uint32_t)__popcll(m0);
@@ -361,7 +464,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 rank1 = h1 ? kq + p0 + b1 : rank1;
                 kq += p0 + (uint32_t)__popcll(m1);
             }
-            uint2* const q = reinterpret_cast<uint2*>(s_img);  // 128 entries, in the image
             if (qd[0]) q[rank0] = make_uint2(ex[0], ey[0]);
             if (qd[1]) q[rank1] = make_uint2(ex[1], ey[1]);
             stamp(3);
@@ -406,7 +508,37 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             uint32_t sX = 0, sO = 0, sSt = 0;
             bool s1 = false;
             stamp(5);
-            if (kMode != 1) {
+            uint32_t Lend = 0;  // the second walk's output end (bytes, image-relative)
+            if (kMode != 1 && dw) {
+                uint32_t* const out32 = reinterpret_cast<uint32_t*>(s_img);
+                const uint32_t dmy32 = dmy >> 2;
+                uint32_t acc = 0, accn = 0;
+                L.o >>= 2;  // (dword indices: the regions start on a dword)
+                N.o >>= 2;
+                for (;;) {
+                    if (kMode == 3) dg[9] += 1;
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) lit12_step_dw(L, acc, accn, win32, s_lut, s_lo, out32, dmy32);
+                    const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
+                    if (__any(fin)) {
+                        const bool sw = fin & nv;
+                        if (sw) {
+                            if (accn) out32[L.o] = acc;  // the first literal's last, partial dword
+                            sX = L.X;
+                            sO = (L.o << 2) + accn;
+                            sSt = L.st;
+                            s1 = L.act;
+                            L = N;
+                            nv = false;
+                            acc = 0;
+                            accn = 0;
+                        }
+                        if (!__any(!fin | sw)) break;
+                    }
+                }
+                if (accn) out32[L.o] = acc;
+                Lend = (L.o << 2) + accn;
+            } else if (kMode != 1) {
                 for (;;) {
                     if (kMode == 3) dg[9] += 1;
 #pragma unroll
@@ -425,18 +557,17 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                         if (!__any(!fin | sw)) break;
                     }
                 }
+                Lend = L.o;
             }
             stamp(6);
             // results: the first slot's from its saved end state, the second's from the walk
-            if (s1) {
+            {
                 const uint32_t Eb = (e1.x & 0xFFFFu) * 8u + 31u + (e1.x >> 16) * 8u;
                 const uint32_t st = sSt != HPK_OK ? sSt : residual_status(Eb - sX, win_at(win32, sX - 31u));
                 rv0 = (sO - ((e1.y >> 12) & 0x1FFFFu)) | (st << 24);
-                ri0 = e1.y & 0xFFFu;
-            }
-            if (L.act) {
-                rv1 = (L.o - L.o0) | (lit12_status(L) << 24);
-                ri1 = L.idx;
+                ri0 = s1 ? e1.y & 0xFFFu : 0xFFFFFFFFu;
+                rv1 = (Lend - L.o0) | (lit12_status(L) << 24);
+                ri1 = L.act ? L.idx : 0xFFFFFFFFu;
             }
             if (kMode == 1) {  // diagnostic: no decode
                 rv0 = 0;

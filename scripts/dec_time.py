@@ -54,7 +54,8 @@ def main():
                       "long_min": os.environ.get("HPK_LONG_MIN", "default"),
                       "lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")),
                       "debug_mode": os.environ.get("HPK_DEBUG_MODE", "0"),
-                      "kernel": os.environ.get("HPK_DECODE_KERNEL", "auto")}), flush=True)
+                      "kernel": os.environ.get("HPK_DECODE_KERNEL", "auto"),
+                      "wave_variant": os.environ.get("HPK_WAVE_VARIANT")}), flush=True)
 
 
 if __name__ == "__main__":
