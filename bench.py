@@ -385,6 +385,9 @@ def main():
     my_enc = sum(w.enc_bytes for w, _ in units)
     my_dec = sum(w.dec_bytes for w, _ in units)
     my_n = sum(w.n for w, _ in units)
+    # bytes of the literals' output regions (the caller's out_off spans: the decoded bound, 8/5 of the
+    # encoded length): the image write-back stores whole spans, the slack past out_len included
+    my_region = sum(int(sets[0][3][-1].item()) & 0xFFFFFFFF for _, sets in units)
     per_step_enc = my_enc if args.workload == "config5" else units[0][0].enc_bytes
 
     def step():
@@ -494,6 +497,22 @@ def main():
         traffic = pm_hbm.get("hbm_bytes_per_launch") if pm_hbm else None
         pm_sq = pmc_summary(os.path.join(args.pmc_dir, f"pmc_sq_{args.workload}.json"), args.workload,
                             lit_per_launch, src)
+        kernel_name = (pm_hbm or pm_sq or {}).get("kernel") or (
+            "hpk_decode_wave" if lit_per_launch >= 4_000_000 else "hpk_decode12")
+        traffic_split = None
+        if pm_hbm and args.workload == "config5":
+            lpl = launches_per_step
+            rd_algo = (my_enc + 8 * my_n) / lpl
+            wr_algo = (my_dec + 5 * my_n) / lpl
+            wr_span = (my_region + 5 * my_n) / lpl
+            traffic_split = {
+                "read_algorithmic": int(rd_algo), "read_pmc": pm_hbm.get("read_bytes_per_launch"),
+                "write_algorithmic": int(wr_algo), "write_region_spans": int(wr_span),
+                "write_pmc": pm_hbm.get("write_bytes_per_launch"),
+                "why": "reads: every fill loads its whole 3 KiB window from a 16-B-aligned start, so the bytes "
+                       "past the fill's last literal are read again by the next fill, and in_off/out_off are "
+                       "read as (t, t+1) pairs; writes: the image write-back stores each fill's whole output span "
+                       "(the regions' slack between out_len and the 8/5 bound included) in 16-B chunks"}
         issue = None
         if pm_sq:
             per = pm_sq["per_launch"]
@@ -544,7 +563,8 @@ def main():
                 "traffic_read": pm_hbm.get("read_bytes_per_launch") if pm_hbm else None,
                 "traffic_write": pm_hbm.get("write_bytes_per_launch") if pm_hbm else None,
                 "issue": issue,
-                "kernel": "hpk_decode12",
+                "kernel": kernel_name,
+                "traffic_vs_algorithmic": traffic_split,
                 "algorithmic_bytes_per_launch": int(algo_per_launch),
                 "literals_per_launch": int(lit_per_launch),
                 "avg_launch_us": round(per_launch_s * 1e6, 3),

@@ -48,16 +48,13 @@ constexpr int kWaveWin = 3072, kWaveImg = 5888;
 #ifndef HPK_WAVE_MIN
 #define HPK_WAVE_MIN 4000000u
 #endif
-#ifndef HPK_WAVE_DW
-#define HPK_WAVE_DW 0  // dword output stores in the wave kernel's lane walk (v25b: 1290 vs 1134 us, off)
-#endif
 #ifndef HPK_WAVE_GUIDED
 #define HPK_WAVE_GUIDED 1  // chunks claimed by the waves (guided self-scheduling) vs a static 1/16 each
 #endif
 #ifndef HPK_WAVE_RANK
 #define HPK_WAVE_RANK 0  // longest-first order: 0 LDS counting sort (32 classes), 1/2 ballots (16/32 classes)
 #endif
-#define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, 224u, HPK_WAVE_DW, HPK_WAVE_GUIDED, HPK_WAVE_RANK>
+#define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, 224u, HPK_WAVE_GUIDED, HPK_WAVE_RANK>
 #define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN>
 
 #ifdef HPK_DIAG
@@ -127,18 +124,16 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     static const int wave_var = getenv("HPK_WAVE_VARIANT") ? atoi(getenv("HPK_WAVE_VARIANT")) : -1;
     if (wave && wave_var >= 0 && g_debug_mode == 0) {
         switch (wave_var) {
-            case 0: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, false, 0>), grid, block, 0, c->stream, a); break;
-            case 1: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, false, 1>), grid, block, 0, c->stream, a); break;
-            case 2: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, false, 2>), grid, block, 0, c->stream, a); break;
-            case 3: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, true, 0>), grid, block, 0, c->stream, a); break;
-            case 4: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, true, 1>), grid, block, 0, c->stream, a); break;
-            case 5: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, true, 2>), grid, block, 0, c->stream, a); break;
-            // window / image split of the same 8960 B per wave, and the least chunk
-            case 6: hipLaunchKernelGGL((hpk_decode_wave<0, 3584, 5376, 224u, false, true, 0>), grid, block, 0, c->stream, a); break;
-            case 7: hipLaunchKernelGGL((hpk_decode_wave<0, 3840, 5120, 224u, false, true, 0>), grid, block, 0, c->stream, a); break;
-            case 8: hipLaunchKernelGGL((hpk_decode_wave<0, 3328, 5632, 224u, false, true, 0>), grid, block, 0, c->stream, a); break;
-            case 9: hipLaunchKernelGGL((hpk_decode_wave<0, 3584, 5376, 128u, false, true, 0>), grid, block, 0, c->stream, a); break;
-            default: hipLaunchKernelGGL((hpk_decode_wave<0, 3584, 5376, 512u, false, true, 0>), grid, block, 0, c->stream, a); break;
+            case 0: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, 0>), grid, block, 0, c->stream, a); break;
+            case 1: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, 1>), grid, block, 0, c->stream, a); break;
+            case 2: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, false, 2>), grid, block, 0, c->stream, a); break;
+            case 3: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, true, 0>), grid, block, 0, c->stream, a); break;
+            case 4: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, true, 1>), grid, block, 0, c->stream, a); break;
+            case 5: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, true, 2>), grid, block, 0, c->stream, a); break;
+            // (the least chunk of the guided hand-out, 128-1024 literals: within the noise, r3l; the 3072 /
+            // 5888 split won over 3328-3840 B windows, whose fourth prefetch round spills, r3i; dword
+            // output by LDS masked OR, bench/legacy_wave_mk.h: 1223-1229 us, r3o)
+            default: hipLaunchKernelGGL((WAVE_KERNEL(0)), grid, block, 0, c->stream, a); break;
         }
         HIP_TRY(hipGetLastError());
         return hpk_long_list_used(c, lslot);

@@ -36,74 +36,6 @@
 
 namespace hpkdec {
 
-// Append g (<= 5) decoded bytes p (little-endian, zero above them) to a lane's pending output (acc,
-// accn <= 3 bytes) and store the dword once it is full: out32[o] (o a dword index), else the lane's
-// dummy dword, so the store is unconditional (no exec-mask branch).
-__device__ __forceinline__ void dw_append(uint32_t& o, uint32_t& acc, uint32_t& accn, uint32_t* __restrict__ out32,
-                                          uint32_t dmy32, uint32_t p, uint32_t g) {
-    const uint64_t x = (uint64_t)p << (8u * accn);
-    const uint32_t lo = acc | (uint32_t)x;
-    const uint32_t n2 = accn + g;
-    const bool full = n2 >= 4u;
-    out32[full ? o : dmy32] = lo;
-    o += full ? 1u : 0u;
-    acc = full ? (uint32_t)(x >> 32) : lo;
-    accn = n2 & 3u;
-}
-
-// lit12_step with dword output (v25b): the step's (up to four) bytes are gathered with v_perm and
-// appended to the lane's pending dword, ONE LDS store per step instead of four byte stores (a
-// literal's region must start and end on a dword). L.o counts dwords; acc / accn are the pending
-// bytes.
-__device__ __forceinline__ void lit12_step_dw(Lit12& L, uint32_t& acc, uint32_t& accn,
-                                              const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
-                                              const uint16_t* __restrict__ lo, uint32_t* __restrict__ out32,
-                                              uint32_t dmy32) {
-    const uint32_t d3 = win32[(L.X >> 5) + 2];
-    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-    const uint32_t rem = L.Eb - L.X;
-    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
-    bool a1, a2;
-    const uint32_t u1 = lut12(e1, rem, a1, a2);
-    bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
-    const bool cont = a1 & (a2 | (e1 >= HPK_LUT2_NOTTWO));
-    const uint32_t w2 = w << u1;
-    const uint32_t rem2 = rem - u1;
-    const uint32_t e2 = lut[w2 >> (32 - HPK_LUT_BITS)];
-    bool b1, b2;
-    const uint32_t u2 = lut12(e2, rem2, b1, b2);
-    park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
-    b1 &= cont;
-    b2 &= cont;
-    const uint32_t g1 = (uint32_t)a1 + (uint32_t)a2, g2 = (uint32_t)b1 + (uint32_t)b2;
-    dw_append(L.o, acc, accn, out32, dmy32, lut12_bytes(e1, g1) | (lut12_bytes(e2, g2) << (8u * g1)), g1 + g2);
-    const uint32_t xn = L.X + u1 + (cont ? u2 : 0u);
-    const bool cross = (xn ^ L.X) > 31u;
-    L.d0 = cross ? L.d1 : L.d0;
-    L.d1 = cross ? L.d2 : L.d1;
-    L.d2 = cross ? d3 : L.d2;
-    L.X = xn;
-    L.prog = a1 | park;
-    if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
-        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-        uint32_t sy, len;
-        bool eos;
-        lo_decode(wp, lo, sy, len, eos);
-        const uint32_t r = L.Eb - L.X;
-        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
-            L.st = HPK_PADDING_TOO_LARGE;
-            L.Eb = L.X;
-        } else if (eos) {  // huffman.rs:112-116
-            L.st = HPK_EOS_IN_STRING;
-            L.Eb = L.X;
-        } else {
-            dw_append(L.o, acc, accn, out32, dmy32, sy, 1u);
-            L.X += len;
-            lit12_load(L, win32);
-        }
-    }
-}
-
 template <int kWinB, int kImgB>
 struct GeoW {
     static constexpr int kWaves = 16, kBlock = kWaves * 64;
@@ -126,7 +58,7 @@ struct GeoW {
 // dense listing found an entry it cannot list, [7] chunks of kChunk literals handed out to the waves
 // kRank: 0 = counting sort with LDS atomics on 32 length classes of 2 bytes, 1 / 2 = ranks from
 // ballots over 16 classes of 4 bytes / 32 classes of 2 bytes (no LDS round trip)
-template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kDw, bool kGuided, int kRank>
+template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank>
 __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     using G = GeoW<kWinB, kImgB>;
     constexpr int kStore = kMode == 2 ? kNoStore : kPred;
@@ -134,13 +66,18 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     // for the fill's offsets + their checks, 2 write-back, 3 queue, 4 window staging, 5 prefetch issue
     // and queue reads, 6 lane loop, 7 byte path + results, 8 fills, 9 lane-loop rounds, 10 long phase,
     // 11 before the first fill
-    unsigned long long dg[12] = {};
-    unsigned long long tq = kMode == 3 ? __builtin_amdgcn_s_memtime() : 0ull;
-    const unsigned long long t_start = tq;
+    // (the sums live in LDS, added by lane 0 with return-less ds_add: held in registers they pushed
+    // the kernel over 128 VGPRs, and the spills' waits distorted what they measured)
+    __shared__ uint32_t s_dg[kMode == 3 ? G::kWaves * 12 : 1];
+    uint32_t tq = kMode == 3 ? (uint32_t)__builtin_amdgcn_s_memtime() : 0u;
+    const uint32_t t_start = tq;
+    auto dg_add = [&](int i, uint32_t v) {
+        if (kMode == 3 && (threadIdx.x & 63u) == 0u) atomicAdd(&s_dg[(threadIdx.x >> 6) * 12u + i], v);
+    };
     auto stamp = [&](int i) {
         if (kMode == 3) {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            dg[i] += t - tq;
+            const uint32_t t = (uint32_t)__builtin_amdgcn_s_memtime();
+            dg_add(i, t - tq);
             tq = t;
         }
     };
@@ -155,6 +92,8 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut2)[t];
     if (tid < 16) s_ctr[tid] = 0;
+    if (kMode == 3)
+        for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
     const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
@@ -321,7 +260,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             // 1. offsets: bounds (bad), what fits
             bool bad = false;
             uint32_t ex[2], ey[2];
-            bool fits[2], unal[2];  // unal: a region that does not start and end on a dword
+            bool fits[2];
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = lane + 64u * r;
@@ -333,11 +272,10 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const bool fast = ocap >= (nbytes * 8u) / 5u;
                 ex[r] = (p0 - base16) | (nbytes << 16);
                 ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
-                unal[r] = fast && ((o0 | ocap) & 3u) != 0u;
             }
             const bool wbad = __any(bad) || stop != 0u;
             stamp(1);
-            if (kMode == 3) dg[8] += 1;
+            dg_add(8, 1u);
             if (wbad) {  // the rest of the wave's chunks is void; nothing more is decoded or written here
                 if (pk) flush();
                 pk = 0;
@@ -417,8 +355,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             // 2. the previous fill's write-back (its image is read out before this fill's queue lands there)
             if (pk) flush();
             stamp(2);
-            // 3. queue, longest first: a rank per literal from ballots over 16 length classes of 4 bytes
-            // (no LDS round trip), long literals listed for the long-literal phase instead
+            // 3. queue, longest first (kRank 0: a counting sort over 32 length classes of 2 bytes, 996-1015
+            // us on config 5 against 1121-1175 us for the ballot ranks, r3h/r3j), long literals listed
+            // for the long-literal phase instead
             bool qd[2];
             uint32_t key[2];
 #pragma unroll
@@ -429,8 +368,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 qd[r] = fits[r] && !lng;
                 key[r] = kRank == 1 ? min(nbytes >> 2, 15u) : min(nbytes >> 1, 31u);
             }
-            // dword output for this fill when every queued literal's region starts and ends on a dword
-            const bool dw = kDw && kStore == kPred && !__any((qd[0] && unal[0]) || (qd[1] && unal[1]));
             uint32_t rank0 = 0, rank1 = 0, kq = 0;
             uint2* const q = reinterpret_cast<uint2*>(s_img + 256);  // 128 entries, in the image
             if (kRank == 0) {  // counting sort: class counts by LDS atomics, bases by a wave scan
@@ -509,38 +446,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             bool s1 = false;
             stamp(5);
             uint32_t Lend = 0;  // the second walk's output end (bytes, image-relative)
-            if (kMode != 1 && dw) {
-                uint32_t* const out32 = reinterpret_cast<uint32_t*>(s_img);
-                const uint32_t dmy32 = dmy >> 2;
-                uint32_t acc = 0, accn = 0;
-                L.o >>= 2;  // (dword indices: the regions start on a dword)
-                N.o >>= 2;
+            if (kMode != 1) {
                 for (;;) {
-                    if (kMode == 3) dg[9] += 1;
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) lit12_step_dw(L, acc, accn, win32, s_lut, s_lo, out32, dmy32);
-                    const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
-                    if (__any(fin)) {
-                        const bool sw = fin & nv;
-                        if (sw) {
-                            if (accn) out32[L.o] = acc;  // the first literal's last, partial dword
-                            sX = L.X;
-                            sO = (L.o << 2) + accn;
-                            sSt = L.st;
-                            s1 = L.act;
-                            L = N;
-                            nv = false;
-                            acc = 0;
-                            accn = 0;
-                        }
-                        if (!__any(!fin | sw)) break;
-                    }
-                }
-                if (accn) out32[L.o] = acc;
-                Lend = (L.o << 2) + accn;
-            } else if (kMode != 1) {
-                for (;;) {
-                    if (kMode == 3) dg[9] += 1;
+                    dg_add(9, 1u);
 #pragma unroll
                     for (int s = 0; s < 2; ++s) lit12_step<kStore>(L, win32, s_lut, s_lo, s_img, dmy);
                     const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
@@ -617,12 +525,12 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                                             reinterpret_cast<uint4*>(area + 512 * (32 * 4 + HPK_LONG_OS)), s_lut, s_lo);
     }
     stamp(10);
-    if (kMode == 3 && lane < 12) {
-        dg[0] = __builtin_amdgcn_s_memtime() - t_start;
-        unsigned long long v = 0;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) v = lane == (uint32_t)i ? dg[i] : v;
-        a.dbg[((uint64_t)blockIdx.x * G::kWaves + wv) * 16u + lane] = v;
+    if (kMode == 3) {
+        __syncthreads();  // (every lane 0's adds are in)
+        if (lane < 12) {
+            const uint32_t v = lane == 0 ? (uint32_t)__builtin_amdgcn_s_memtime() - t_start : s_dg[wv * 12u + lane];
+            a.dbg[((uint64_t)blockIdx.x * G::kWaves + wv) * 16u + lane] = v;
+        }
     }
 }
 
