@@ -74,11 +74,27 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     return c;
 }
 
+// The long-literal list of a launch: one slot per stream (a stream's launches are ordered, so its
+// slot is reused without a wait). Completion events are recorded only once a second stream has used
+// the context (an event record per launch cost ~1 us of a ~23 us small call); from then on a slot
+// taken over by another stream, or grown, waits for its last launch.
 int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
     int j = -1;
-    for (int k = 0; k < hpk_ctx::kLongSlots; ++k)
+    bool any = false;
+    for (int k = 0; k < hpk_ctx::kLongSlots; ++k) {
         if (c->long_list[k] && c->long_stream[k] == c->stream) j = k;
+        any |= c->long_list[k] != nullptr;
+    }
     if (j < 0) {
+        if (any && !c->long_multi) {  // a second stream: events from here on, and one for the past
+            c->long_multi = true;
+            for (int k = 0; k < hpk_ctx::kLongSlots; ++k) {
+                if (!c->long_list[k]) continue;
+                if (!c->long_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[k], hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(c->long_ev[k], c->long_stream[k]));
+                c->long_ev_set[k] = true;
+            }
+        }
         j = 0;
         while (j < hpk_ctx::kLongSlots && c->long_list[j]) ++j;
         if (j == hpk_ctx::kLongSlots) {  // all taken: reuse the oldest once its last launch is done
@@ -88,9 +104,12 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
         }
         c->long_stream[j] = c->stream;
     }
-    if (!c->long_ev[j]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[j], hipEventDisableTiming));
+    if (c->long_multi && !c->long_ev[j]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[j], hipEventDisableTiming));
     if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
-        if (c->long_ev_set[j]) HIP_TRY(hipEventSynchronize(c->long_ev[j]));
+        if (c->long_ev_set[j])
+            HIP_TRY(hipEventSynchronize(c->long_ev[j]));
+        else if (c->long_list[j])
+            HIP_TRY(hipStreamSynchronize(c->long_stream[j]));
         (void)hipFree(c->long_list[j]);
         c->long_list[j] = nullptr;
         c->long_list_cap[j] = 0;
@@ -104,6 +123,7 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
 }
 
 int hpk_long_list_used(hpk_ctx* c, int slot) {
+    if (!c->long_multi) return HPK_E_OK;
     HIP_TRY(hipEventRecord(c->long_ev[slot], c->stream));
     c->long_ev_set[slot] = true;
     return HPK_E_OK;
@@ -132,6 +152,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
         if (c->ev_in[j]) (void)hipEventDestroy(c->ev_in[j]);
         if (c->ev_run[j]) (void)hipEventDestroy(c->ev_run[j]);
+        if (c->ev_out[j]) (void)hipEventDestroy(c->ev_out[j]);
     }
     if (c->h2d) (void)hipStreamDestroy(c->h2d);
     if (c->d2h) (void)hipStreamDestroy(c->d2h);
@@ -228,6 +249,84 @@ typedef int (*launch_fn)(hpk_ctx*, const hpk_batch&);
 
 static uint32_t clamp_cap(size_t cap) { return cap > HPK_MAX_OFFSET ? HPK_MAX_OFFSET : (uint32_t)cap; }
 
+// Host-pointer batches: stage, run and copy back, cut into up to kMaxChunks literal ranges balanced
+// by encoded bytes; chunk j's copy-in (h2d stream), kernel (ctx stream) and copy-out (d2h stream)
+// overlap with the neighbouring chunks' (PCIe is full duplex), and ev_out[j] marks its results in
+// host memory. Offsets stay absolute, so every chunk is the same kernel on a sub-range of the
+// scratch buffers. With pageable host memory HIP stages the copies itself and the overlap is small:
+// register the arena (hpk_host_register). `trusted`: the offsets were made by the library itself
+// (hpk_hdec_decode_blocks), monotone by construction, so the O(n) host checks are skipped.
+static int host_begin(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
+                      uint32_t n, uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
+                      uint8_t* status, bool trusted, int* nchunks, uint32_t* cut) {
+    *nchunks = 0;
+    if (!trusted && (check_offsets(in_off, n, in_cap) || check_offsets(out_off, n, out_cap))) return HPK_E_INVAL;
+    if (n == 0) return HPK_E_OK;
+    const size_t in_bytes = in_off[n], out_bytes = out_off[n];
+    if ((in_bytes && !in_blob) || (out_bytes && !out_blob)) return hpk_set_err_msg("null blob", HPK_E_INVAL);
+    int rc;
+    if ((rc = grow((void**)&c->d_in, &c->d_in_cap, in_bytes + 16))) return rc;
+    if ((rc = grow((void**)&c->d_out, &c->d_out_cap, out_bytes + 16))) return rc;
+    if ((rc = grow((void**)&c->d_meta, &c->d_meta_cap, (3 * (size_t)n + 2) * 4))) return rc;
+    if ((rc = grow((void**)&c->d_st, &c->d_st_cap, n))) return rc;
+    uint32_t* d_in_off = c->d_meta;
+    uint32_t* d_out_off = c->d_meta + (n + 1);
+    uint32_t* d_len = c->d_meta + 2 * ((size_t)n + 1);
+    if (!c->h2d) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
+        for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_in[j], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_run[j], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_out[j], hipEventDisableTiming));
+        }
+    }
+    const size_t kChunkBytes = (size_t)4 << 20;
+    int chunks = (int)((in_bytes + out_bytes) / kChunkBytes);
+    chunks = chunks < 1 ? 1 : (chunks > hpk_ctx::kMaxChunks ? hpk_ctx::kMaxChunks : chunks);
+    if ((uint32_t)chunks > n) chunks = (int)n;
+    cut[0] = 0;
+    for (int j = 1; j < chunks; ++j) {  // first literal whose end passes j/chunks of the bytes
+        const uint64_t target = (uint64_t)in_bytes * j / chunks;
+        uint32_t lo = cut[j - 1], hi = n;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (in_off[mid + 1] < target) lo = mid + 1; else hi = mid;
+        }
+        cut[j] = lo;
+    }
+    cut[chunks] = n;
+    HIP_TRY(hipEventRecord(c->ev_run[0], c->stream));  // earlier work on the ctx stream first
+    HIP_TRY(hipStreamWaitEvent(c->h2d, c->ev_run[0], 0));
+    for (int j = 0; j < chunks; ++j) {
+        const uint32_t a = cut[j], b = cut[j + 1];
+        if (a < b) {
+            const size_t ib = in_off[a], ie = in_off[b], ob = out_off[a], oe = out_off[b];
+            if (ie > ib) HIP_TRY(hipMemcpyAsync(c->d_in + ib, in_blob + ib, ie - ib, hipMemcpyHostToDevice, c->h2d));
+            HIP_TRY(hipMemcpyAsync(d_in_off + a, in_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
+            HIP_TRY(hipMemcpyAsync(d_out_off + a, out_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
+            HIP_TRY(hipEventRecord(c->ev_in[j], c->h2d));
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_in[j], 0));
+            const hpk_batch bt{c->d_in, (uint32_t)in_bytes, d_in_off + a, b - a, c->d_out, (uint32_t)out_bytes,
+                               d_out_off + a, d_len + a, c->d_st + a};
+            if ((rc = fn(c, bt))) return rc;
+            HIP_TRY(hipEventRecord(c->ev_run[j], c->stream));
+            HIP_TRY(hipStreamWaitEvent(c->d2h, c->ev_run[j], 0));
+            if (oe > ob) HIP_TRY(hipMemcpyAsync(out_blob + ob, c->d_out + ob, oe - ob, hipMemcpyDeviceToHost, c->d2h));
+            HIP_TRY(hipMemcpyAsync(out_len + a, d_len + a, (b - a) * 4ull, hipMemcpyDeviceToHost, c->d2h));
+            HIP_TRY(hipMemcpyAsync(status + a, c->d_st + a, b - a, hipMemcpyDeviceToHost, c->d2h));
+        }
+        HIP_TRY(hipEventRecord(c->ev_out[j], c->d2h));
+    }
+    *nchunks = chunks;
+    return HPK_E_OK;
+}
+
+static int host_end(hpk_ctx* c) {
+    HIP_TRY(hipStreamSynchronize(c->d2h));
+    return take_err(c);
+}
+
 static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
                      uint32_t n, uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                      uint8_t* status, int flags) {
@@ -245,71 +344,33 @@ static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in
         }
         return HPK_E_OK;
     }
-    // host pointers: validate, stage, run, copy back
-    if (check_offsets(in_off, n, in_cap) || check_offsets(out_off, n, out_cap)) return HPK_E_INVAL;
-    if (n == 0) return HPK_E_OK;
-    const size_t in_bytes = in_off[n], out_bytes = out_off[n];
-    if ((in_bytes && !in_blob) || (out_bytes && !out_blob)) return hpk_set_err_msg("null blob", HPK_E_INVAL);
-    int rc;
-    if ((rc = grow((void**)&c->d_in, &c->d_in_cap, in_bytes + 16))) return rc;
-    if ((rc = grow((void**)&c->d_out, &c->d_out_cap, out_bytes + 16))) return rc;
-    if ((rc = grow((void**)&c->d_meta, &c->d_meta_cap, (3 * (size_t)n + 2) * 4))) return rc;
-    if ((rc = grow((void**)&c->d_st, &c->d_st_cap, n))) return rc;
-    uint32_t* d_in_off = c->d_meta;
-    uint32_t* d_out_off = c->d_meta + (n + 1);
-    uint32_t* d_len = c->d_meta + 2 * ((size_t)n + 1);
-    // Pipeline: the batch is cut into up to kMaxChunks literal ranges balanced by encoded bytes;
-    // chunk j's copy-in (h2d stream), kernel (ctx stream) and copy-out (d2h stream) overlap with
-    // the neighbouring chunks' (PCIe is full duplex). Offsets stay absolute, so every chunk is
-    // the same kernel on a sub-range of the scratch buffers. With pageable host memory HIP
-    // stages the copies itself and the overlap is small: register the arena (hpk_host_register).
-    if (!c->h2d) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
-        for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_in[j], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_run[j], hipEventDisableTiming));
-        }
-    }
-    const size_t kChunkBytes = (size_t)4 << 20;
-    int chunks = (int)((in_bytes + out_bytes) / kChunkBytes);
-    chunks = chunks < 1 ? 1 : (chunks > hpk_ctx::kMaxChunks ? hpk_ctx::kMaxChunks : chunks);
-    if ((uint32_t)chunks > n) chunks = (int)n;
+    int chunks;
     uint32_t cut[hpk_ctx::kMaxChunks + 1];
-    cut[0] = 0;
-    for (int j = 1; j < chunks; ++j) {  // first literal whose end passes j/chunks of the bytes
-        const uint64_t target = (uint64_t)in_bytes * j / chunks;
-        uint32_t lo = cut[j - 1], hi = n;
-        while (lo < hi) {
-            const uint32_t mid = lo + (hi - lo) / 2;
-            if (in_off[mid + 1] < target) lo = mid + 1; else hi = mid;
-        }
-        cut[j] = lo;
-    }
-    cut[chunks] = n;
-    HIP_TRY(hipEventRecord(c->ev_run[0], c->stream));  // earlier work on the ctx stream first
-    HIP_TRY(hipStreamWaitEvent(c->h2d, c->ev_run[0], 0));
-    for (int j = 0; j < chunks; ++j) {
-        const uint32_t a = cut[j], b = cut[j + 1];
-        if (a == b) continue;
-        const size_t ib = in_off[a], ie = in_off[b], ob = out_off[a], oe = out_off[b];
-        if (ie > ib) HIP_TRY(hipMemcpyAsync(c->d_in + ib, in_blob + ib, ie - ib, hipMemcpyHostToDevice, c->h2d));
-        HIP_TRY(hipMemcpyAsync(d_in_off + a, in_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
-        HIP_TRY(hipMemcpyAsync(d_out_off + a, out_off + a, (b - a + 1) * 4ull, hipMemcpyHostToDevice, c->h2d));
-        HIP_TRY(hipEventRecord(c->ev_in[j], c->h2d));
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_in[j], 0));
-        const hpk_batch bt{c->d_in, (uint32_t)in_bytes, d_in_off + a, b - a, c->d_out, (uint32_t)out_bytes,
-                           d_out_off + a, d_len + a, c->d_st + a};
-        if ((rc = fn(c, bt))) return rc;
-        HIP_TRY(hipEventRecord(c->ev_run[j], c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->d2h, c->ev_run[j], 0));
-        if (oe > ob) HIP_TRY(hipMemcpyAsync(out_blob + ob, c->d_out + ob, oe - ob, hipMemcpyDeviceToHost, c->d2h));
-        HIP_TRY(hipMemcpyAsync(out_len + a, d_len + a, (b - a) * 4ull, hipMemcpyDeviceToHost, c->d2h));
-        HIP_TRY(hipMemcpyAsync(status + a, c->d_st + a, b - a, hipMemcpyDeviceToHost, c->d2h));
-    }
-    HIP_TRY(hipStreamSynchronize(c->d2h));
-    return take_err(c);
+    if (int rc = host_begin(fn, c, in_blob, in_cap, in_off, n, out_blob, out_cap, out_off, out_len, status, false,
+                            &chunks, cut))
+        return rc;
+    return chunks ? host_end(c) : HPK_E_OK;
 }
+
+// The block decoder's form (hpk_hpack.cpp): a trusted host batch started here, its chunks' results
+// waited for one by one (so the caller applies chunk j's blocks while later chunks still decode),
+// then finished. Not part of the C ABI.
+int hpk_decode_host_begin(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
+                          uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
+                          uint8_t* status, int* nchunks, uint32_t* cut) {
+    HIP_TRY(hipSetDevice(c->device));
+    return host_begin(hpk_launch_decode, c, in_blob, in_cap, in_off, n, out_blob, out_cap, out_off, out_len, status,
+                      true, nchunks, cut);
+}
+
+int hpk_host_chunk_wait(hpk_ctx* c, int j) {
+    HIP_TRY(hipEventSynchronize(c->ev_out[j]));
+    return HPK_E_OK;
+}
+
+int hpk_decode_host_end(hpk_ctx* c) { return host_end(c); }
+
+int hpk_ctx_max_chunks() { return hpk_ctx::kMaxChunks; }
 
 extern "C" int hpk_decode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
                                 uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,

@@ -38,6 +38,7 @@ struct hpk_ctx {
     hipStream_t d2h = nullptr;
     hipEvent_t ev_in[kMaxChunks] = {};
     hipEvent_t ev_run[kMaxChunks] = {};
+    hipEvent_t ev_out[kMaxChunks] = {};  // chunk j's results are in host memory
     // sticky error flag: host-mapped, written (plain store of 1) by a kernel that saw bad offsets
     uint32_t* h_err = nullptr;
     uint32_t* d_err = nullptr;
@@ -52,6 +53,7 @@ struct hpk_ctx {
     uint32_t* long_list[kLongSlots] = {};
     size_t long_list_cap[kLongSlots] = {};
     int long_next = 0;
+    bool long_multi = false;  // more than one stream has used the context: slots carry events
 };
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on

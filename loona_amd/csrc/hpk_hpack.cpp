@@ -17,8 +17,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <deque>
+#include <functional>
+#include <mutex>
 #include <unordered_map>
 #include <thread>
 #include <string>
@@ -29,6 +33,13 @@
 int hpk_set_err_msg(const char* what, int code);  // hpk_ctx.hip: hpk_last_error's message
 // hpk_ctx.hip: the context's page-locked host staging area, grown to at least `bytes` (grow-only)
 int hpk_ctx_pinned(hpk_ctx* ctx, size_t bytes, void** p);
+// hpk_ctx.hip: a trusted host batch whose chunks can be waited for one by one (not in the C ABI)
+int hpk_decode_host_begin(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,
+                          uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
+                          uint8_t* status, int* nchunks, uint32_t* cut);
+int hpk_host_chunk_wait(hpk_ctx* c, int j);
+int hpk_decode_host_end(hpk_ctx* c);
+int hpk_ctx_max_chunks();
 
 namespace {
 
@@ -97,6 +108,96 @@ const char* const kStatic[61][2] = {
     {"www-authenticate", ""},
 };
 
+uint32_t static_len(int i, int part) {  // strlen of kStatic[i][part], computed once
+    static const auto lens = [] {
+        std::vector<uint32_t> v(122);
+        for (int k = 0; k < 61; ++k) {
+            v[2 * k] = (uint32_t)strlen(kStatic[k][0]);
+            v[2 * k + 1] = (uint32_t)strlen(kStatic[k][1]);
+        }
+        return v;
+    }();
+    return lens[2 * i + part];
+}
+
+// A fixed set of worker threads for the block calls' parallel passes (spawning 15 threads per
+// pass cost more than a small pass). One call at a time uses it; a concurrent caller (loona's
+// runtime threads each decode their own connections) spawns its own threads instead.
+class Pool {
+  public:
+    static constexpr int kMax = 16;
+    // fn(t) for t in [0, n): t = 0 on the calling thread
+    void run(int n, const std::function<void(int)>& fn) {
+        if (n <= 1) {
+            fn(0);
+            return;
+        }
+        std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
+        if (!busy.owns_lock()) {  // in use by another caller
+            std::vector<std::thread> th;
+            for (int t = 1; t < n; ++t) th.emplace_back(fn, t);
+            fn(0);
+            for (auto& x : th) x.join();
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            while ((int)th_.size() < kMax - 1) {
+                const int id = (int)th_.size() + 1;
+                th_.emplace_back([this, id] { work(id); });
+            }
+            job_ = &fn;
+            n_ = n;
+            pending_ = n - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& x : th_) x.join();
+    }
+
+  private:
+    void work(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= n_) continue;
+                job = job_;
+            }
+            (*job)(id);
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex use_, m_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> th_;
+    const std::function<void(int)>* job_ = nullptr;
+    int n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+Pool& pool() {
+    static Pool p;
+    return p;
+}
+
 // decode_integer (decoder.rs:67-125): prefix 1..8, at most 5 octets.
 int decode_integer(const uint8_t* p, size_t n, int prefix, uint64_t* value, size_t* consumed) {
     if (prefix < 1 || prefix > 8) return HPK_BLK_INT_INVALID_PREFIX;
@@ -126,10 +227,11 @@ int decode_integer(const uint8_t* p, size_t n, int prefix, uint64_t* value, size
 }
 
 struct Str {
-    uint32_t off = 0;  // absolute offset of the string bytes in the blocks buffer
-    uint32_t len = 0;
-    bool huff = false;
-    uint32_t lit = 0;  // index in the Huffman batch (huff only)
+    uint32_t off;       // absolute offset of the string bytes in the blocks buffer
+    uint32_t len;
+    uint32_t lit : 31;  // index among its scan thread's Huffman strings (huff only; + that thread's base)
+    uint32_t huff : 1;
+    Str() : off(0), len(0), lit(0), huff(0) {}
 };
 
 enum Kind : uint8_t { kIndexed, kLitIncr, kSizeUpdate, kLitNever, kLitPlain };
@@ -138,16 +240,18 @@ enum Kind : uint8_t { kIndexed, kLitIncr, kSizeUpdate, kLitNever, kLitPlain };
 // the reference would have raised it.
 enum Stage : uint8_t { kStIndex = 0, kStName = 1, kStValue = 2 };
 
-struct Field {
-    Kind kind;
+struct Field {  // 40 bytes: a batch's fields are written once by the scan and read once by the apply
     uint64_t index = 0;  // header index / name index / new table size
     Str name, value;
-    int err = HPK_BLK_OK;  // scan error in this field (the last field scanned)
+    int8_t err = HPK_BLK_OK;  // scan error in this field (the last field scanned)
+    Kind kind = kIndexed;
     Stage err_stage = kStIndex;
 };
+static_assert(sizeof(Field) <= 40, "Field packing");
 
 struct Scan {  // a block's fields: pools[pool][first .. first + n) (one field pool per host thread)
     uint32_t pool = 0, first = 0, n = 0;
+    uint32_t lit_end = 0;  // its scan thread's Huffman strings so far, this block's included
 };
 
 // decode_string's framing (decoder.rs:135-163) without the Huffman step.
@@ -159,7 +263,7 @@ int scan_string(const uint8_t* base, size_t pos, size_t end, Str* s, size_t* con
     if (c + len > end - pos) return HPK_BLK_STR_NOT_ENOUGH_OCTETS;
     s->off = (uint32_t)(pos + c);
     s->len = (uint32_t)len;
-    s->huff = (base[pos] & 128u) != 0;
+    s->huff = (base[pos] & 128u) ? 1u : 0u;
     *consumed = c + (size_t)len;
     return HPK_BLK_OK;
 }
@@ -173,6 +277,7 @@ void scan_block(const uint8_t* base, size_t begin, size_t end, uint32_t pool_id,
     out->first = (uint32_t)pool->size();
     scan_fields(base, begin, end, pool, hoff, hlen);
     out->n = (uint32_t)pool->size() - out->first;
+    out->lit_end = (uint32_t)hoff->size();
 }
 
 void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Field>* pool, std::vector<uint32_t>* hoff,
@@ -190,7 +295,7 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
         f.kind = (b & 128u) ? kIndexed : (b & 64u) ? kLitIncr : (b & 32u) ? kSizeUpdate : (b & 16u) ? kLitNever : kLitPlain;
         size_t c = 0;
         if (f.kind == kIndexed || f.kind == kSizeUpdate) {
-            f.err = decode_integer(base + pos, end - pos, f.kind == kIndexed ? 7 : 5, &f.index, &c);
+            f.err = (int8_t)decode_integer(base + pos, end - pos, f.kind == kIndexed ? 7 : 5, &f.index, &c);
             pool->push_back(f);
             if (f.err) return;
             pos += c;
@@ -198,7 +303,7 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
         }
         // decode_literal (decoder.rs:502-527)
         const int prefix = f.kind == kLitIncr ? 6 : 4;
-        f.err = decode_integer(base + pos, end - pos, prefix, &f.index, &c);
+        f.err = (int8_t)decode_integer(base + pos, end - pos, prefix, &f.index, &c);
         if (f.err) {
             pool->push_back(f);
             return;
@@ -206,7 +311,7 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
         size_t at = pos + c;
         if (f.index == 0) {
             size_t cn;
-            f.err = scan_string(base, at, end, &f.name, &cn);
+            f.err = (int8_t)scan_string(base, at, end, &f.name, &cn);
             if (f.err) {
                 f.err_stage = kStName;
                 pool->push_back(f);
@@ -216,7 +321,7 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
             at += cn;
         }
         size_t cv;
-        f.err = scan_string(base, at, end, &f.value, &cv);
+        f.err = (int8_t)scan_string(base, at, end, &f.value, &cv);
         if (f.err) {
             f.err_stage = kStValue;
             pool->push_back(f);
@@ -232,43 +337,85 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
 }  // namespace
 
 // Decoder state: the dynamic table (lib.rs:43-164) and the SizeUpdate limit (decoder.rs:316-318).
+// The table holds its entries' bytes in one buffer, appended at the end, and the entries (offset,
+// name length, value length) in a ring, newest first: an insertion or eviction allocates nothing
+// (the reference's VecDeque of owned strings allocates per entry). Evicted bytes are reclaimed by
+// moving the live ones (at most max_size bytes) to the buffer's start when the end is reached.
 struct hpk_hdec {
-    std::deque<std::pair<std::string, std::string>> table;  // front = newest
+    struct Ent {
+        uint32_t at, nl, vl;
+    };
+    std::vector<Ent> ring{std::vector<Ent>(64)};  // capacity a power of two
+    uint32_t first = 0, count = 0;                // newest entry at ring[first]
+    std::vector<uint8_t> bytes;
+    size_t end = 0;                               // bytes[0, end): entries' names and values
     size_t size = 0;
     size_t max_size = 4096;
     bool has_max_allowed = false;
     size_t max_allowed = 0;
 
-    void consolidate() {
-        while (size > max_size) {
-            const auto& last = table.back();
-            size -= last.first.size() + last.second.size() + 32;
-            table.pop_back();
-        }
+    const Ent& at(size_t di) const { return ring[(first + di) & (ring.size() - 1)]; }
+    void pop_oldest() {
+        const Ent& e = at(count - 1);
+        size -= (size_t)e.nl + e.vl + 32;
+        count -= 1;
+        if (count == 0) end = 0;
     }
-    void add(std::string n, std::string v) {
-        size += n.size() + v.size() + 32;
-        table.emplace_front(std::move(n), std::move(v));
-        consolidate();
+    void consolidate() {
+        while (size > max_size) pop_oldest();
+    }
+    // add_header then consolidate (lib.rs:97-117): an entry larger than the limit empties the
+    // table. n and v must not point into the table.
+    void add(const uint8_t* n, size_t nl, const uint8_t* v, size_t vl) {
+        const size_t sz = nl + vl + 32;
+        if (sz > max_size) {
+            count = 0;
+            size = 0;
+            end = 0;
+            return;
+        }
+        while (size + sz > max_size) pop_oldest();
+        if (end + nl + vl > bytes.size()) {
+            const size_t lo = count ? at(count - 1).at : end;  // the oldest live byte
+            if (lo) {
+                memmove(bytes.data(), bytes.data() + lo, end - lo);
+                for (uint32_t k = 0; k < count; ++k) ring[(first + k) & (ring.size() - 1)].at -= (uint32_t)lo;
+                end -= lo;
+            }
+            if (end + nl + vl > bytes.size()) bytes.resize(std::max<size_t>(2 * (end + nl + vl), 8192));
+        }
+        if (count == ring.size()) {  // grow the ring, newest first at 0
+            std::vector<Ent> r(2 * ring.size());
+            for (uint32_t k = 0; k < count; ++k) r[k] = at(k);
+            ring.swap(r);
+            first = 0;
+        }
+        if (nl) memcpy(bytes.data() + end, n, nl);
+        if (vl) memcpy(bytes.data() + end + nl, v, vl);
+        first = (first - 1) & (uint32_t)(ring.size() - 1);
+        ring[first] = Ent{(uint32_t)end, (uint32_t)nl, (uint32_t)vl};
+        count += 1;
+        end += nl + vl;
+        size += sz;
     }
     // HeaderTable::get_from_table (lib.rs:228-255): 1-based, static then dynamic
-    bool get(uint64_t index, const char** n, size_t* nl, const char** v, size_t* vl) const {
+    bool get(uint64_t index, const uint8_t** n, size_t* nl, const uint8_t** v, size_t* vl) const {
         if (index == 0) return false;
         const uint64_t ri = index - 1;
         if (ri < 61) {
-            *n = kStatic[ri][0];
-            *nl = strlen(*n);
-            *v = kStatic[ri][1];
-            *vl = strlen(*v);
+            *n = (const uint8_t*)kStatic[ri][0];
+            *nl = static_len((int)ri, 0);
+            *v = (const uint8_t*)kStatic[ri][1];
+            *vl = static_len((int)ri, 1);
             return true;
         }
         const uint64_t di = ri - 61;
-        if (di >= table.size()) return false;
-        const auto& e = table[(size_t)di];
-        *n = e.first.data();
-        *nl = e.first.size();
-        *v = e.second.data();
-        *vl = e.second.size();
+        if (di >= count) return false;
+        const Ent& e = at((size_t)di);
+        *n = bytes.data() + e.at;
+        *nl = e.nl;
+        *v = bytes.data() + e.at + e.nl;
+        *vl = e.vl;
         return true;
     }
 };
@@ -295,22 +442,37 @@ extern "C" int hpk_hdec_set_max_allowed_table_size(hpk_hdec* d, size_t n) {
 extern "C" int hpk_hdec_table_size(const hpk_hdec* d, size_t* size, size_t* entries, size_t* max_size) {
     if (!d) return HPK_E_INVAL;
     if (size) *size = d->size;
-    if (entries) *entries = d->table.size();
+    if (entries) *entries = d->count;
     if (max_size) *max_size = d->max_size;
     return HPK_E_OK;
 }
 
 namespace {
 
+// A thread's output: header bytes and header records appended with plain copies (the vectors' sizes
+// are capacities; vector::insert per string cost a fifth of the apply pass).
 struct Out {
     std::vector<uint8_t> arena;
     std::vector<hpk_header> headers;
+    size_t an = 0, hn = 0;  // bytes / records in use
+    void reset(size_t abytes, size_t nhdr) {
+        an = hn = 0;
+        if (arena.size() < abytes) arena.resize(abytes);
+        if (headers.size() < nhdr) headers.resize(nhdr);
+    }
 };
 
-uint32_t put(Out& o, const void* p, size_t n) {
-    const uint32_t at = (uint32_t)o.arena.size();
-    o.arena.insert(o.arena.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+inline uint32_t put(Out& o, const void* p, size_t n) {
+    const uint32_t at = (uint32_t)o.an;
+    if (o.an + n > o.arena.size()) o.arena.resize(std::max(2 * o.arena.size(), o.an + n + 4096));
+    if (n) memcpy(o.arena.data() + o.an, p, n);
+    o.an += n;
     return at;
+}
+
+inline void put_header(Out& o, const hpk_header& h) {
+    if (o.hn == o.headers.size()) o.headers.resize(2 * o.headers.size() + 1024);
+    o.headers[o.hn++] = h;
 }
 
 struct Huff {  // the Huffman batch's results (host memory: pageable vectors or the ctx's pinned area)
@@ -318,13 +480,15 @@ struct Huff {  // the Huffman batch's results (host memory: pageable vectors or 
     const uint32_t* oo;
     const uint32_t* len;
     const uint8_t* st;
+    const uint32_t* lbase;  // batch index of each scan thread's first string
 };
 
 // Pass 3 for one block: the reference's single pass over the scanned fields.
 void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const std::vector<std::vector<Field>>& pools,
                  const Huff& h, Out& o, hpk_block_result* r) {
     const Field* fields = pools[sc.pool].data() + sc.first;
-    r->first_header = (uint32_t)o.headers.size();
+    const uint32_t lb = h.lbase[sc.pool];
+    r->first_header = (uint32_t)o.hn;
     r->n_headers = 0;
     r->error = HPK_BLK_OK;
     r->detail = 0;
@@ -335,30 +499,34 @@ void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const std::ve
     // string bytes: raw from the block, Huffman from the batch (status checked by the caller)
     auto str = [&](const Str& s, const uint8_t** p, size_t* n) {
         if (s.huff) {
-            *p = h.out + h.oo[s.lit];
-            *n = h.len[s.lit];
+            *p = h.out + h.oo[lb + s.lit];
+            *n = h.len[lb + s.lit];
         } else {
             *p = base + s.off;
             *n = s.len;
         }
     };
-    auto huff_err = [&](const Str& s) -> int { return s.huff ? h.st[s.lit] : 0; };
+    auto huff_err = [&](const Str& s) -> int { return s.huff ? h.st[lb + s.lit] : 0; };
+    auto emit = [&](const uint8_t* n, size_t nl, const uint8_t* v, size_t vl) {  // -> the header's index
+        hpk_header hd;
+        hd.name_len = (uint32_t)nl;
+        hd.name_off = put(o, n, nl);
+        hd.value_len = (uint32_t)vl;
+        hd.value_off = put(o, v, vl);
+        put_header(o, hd);
+        r->n_headers += 1;
+        return hd;
+    };
     bool last_was_size_update = false;
     for (size_t fi = 0; fi < sc.n; ++fi) {
         const Field& f = fields[fi];
         last_was_size_update = f.kind == kSizeUpdate;
         if (f.err && f.err_stage == kStIndex) return fail(f.err, 0);
         if (f.kind == kIndexed) {
-            const char *n, *v;
+            const uint8_t *n, *v;
             size_t nl, vl;
             if (!d->get(f.index, &n, &nl, &v, &vl)) return fail(HPK_BLK_HEADER_INDEX_OUT_OF_BOUNDS, 0);
-            hpk_header hd;
-            hd.name_len = (uint32_t)nl;
-            hd.name_off = put(o, n, nl);
-            hd.value_len = (uint32_t)vl;
-            hd.value_off = put(o, v, vl);
-            o.headers.push_back(hd);
-            r->n_headers += 1;
+            emit(n, nl, v, vl);
             continue;
         }
         if (f.kind == kSizeUpdate) {  // update_max_dynamic_size (decoder.rs:538-554)
@@ -370,31 +538,25 @@ void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const std::ve
         // literal: name (literal string or table name), then value
         const uint8_t* np;
         size_t nl;
-        std::string name_store;
         if (f.index == 0) {
             if (f.err && f.err_stage == kStName) return fail(f.err, 0);
             if (int hs = huff_err(f.name)) return fail(HPK_BLK_STR_HUFFMAN, hs);
             str(f.name, &np, &nl);
         } else {
-            const char *n, *v;
+            const uint8_t* v;
             size_t vl;
-            if (!d->get(f.index, &n, &nl, &v, &vl)) return fail(HPK_BLK_HEADER_INDEX_OUT_OF_BOUNDS, 0);
-            name_store.assign(n, nl);  // the insertion below may evict the entry it points into
-            np = (const uint8_t*)name_store.data();
+            if (!d->get(f.index, &np, &nl, &v, &vl)) return fail(HPK_BLK_HEADER_INDEX_OUT_OF_BOUNDS, 0);
         }
         if (f.err && f.err_stage == kStValue) return fail(f.err, 0);
         if (int hs = huff_err(f.value)) return fail(HPK_BLK_STR_HUFFMAN, hs);
         const uint8_t* vp;
         size_t vl;
         str(f.value, &vp, &vl);
-        hpk_header hd;
-        hd.name_len = (uint32_t)nl;
-        hd.name_off = put(o, np, nl);
-        hd.value_len = (uint32_t)vl;
-        hd.value_off = put(o, vp, vl);
-        o.headers.push_back(hd);
-        r->n_headers += 1;
-        if (f.kind == kLitIncr) d->add(std::string((const char*)np, nl), std::string((const char*)vp, vl));
+        const hpk_header hd = emit(np, nl, vp, vl);
+        // the insertion reads the header's copies in the output (the table name it came from may be
+        // evicted by the insertion itself)
+        if (f.kind == kLitIncr)
+            d->add(o.arena.data() + hd.name_off, nl, o.arena.data() + hd.value_off, vl);
     }
     if (last_was_size_update) fail(HPK_BLK_SIZE_UPDATE_AT_END, 0);
 }
@@ -402,6 +564,39 @@ void apply_block(hpk_hdec* d, const uint8_t* base, const Scan& sc, const std::ve
 }  // namespace
 
 namespace {
+// The output buffers of the last freed hpk_blocks_out (hpk_blocks_out_free), handed to the next
+// call that fits in them: the caller-owned results are large (tens of MB for a big batch), and a
+// fresh malloc of that size is a fresh mapping whose every page faults on first write.
+struct OutCache {
+    std::mutex m;
+    void* p[3] = {};
+    size_t cap[3] = {};  // bytes
+    void* take(int k, size_t bytes) {
+        {
+            std::lock_guard<std::mutex> g(m);
+            if (p[k] && cap[k] >= bytes) {
+                void* r = p[k];
+                p[k] = nullptr;
+                cap[k] = 0;
+                return r;
+            }
+        }
+        return malloc(bytes ? bytes : 1);
+    }
+    void give(int k, void* q, size_t bytes) {
+        if (!q) return;
+        std::lock_guard<std::mutex> g(m);
+        if (!p[k] || bytes > cap[k]) {
+            free(p[k]);
+            p[k] = q;
+            cap[k] = bytes;
+        } else {
+            free(q);
+        }
+    }
+};
+OutCache g_out_cache;  // [0] arena, [1] headers, [2] block results
+
 // Scratch of hpk_hdec_decode_blocks, kept per calling thread (loona calls from its runtime
 // threads; each keeps its own): steady-state calls reuse capacity instead of page-faulting
 // fresh allocations in every pass.
@@ -410,12 +605,17 @@ struct BlockScratch {
     std::vector<std::vector<Field>> pools;
     std::vector<std::vector<uint32_t>> thoff, thlen;
     std::vector<uint32_t> lbase, in_off, out_off, len, abase, hbase;
+    std::vector<uint64_t> tin, tout;
     std::vector<uint8_t> st, in, dec, owner;
     std::vector<Out> outs;
 };
 thread_local BlockScratch t_scratch;
 }  // namespace
 
+// Timeline of a call with a device context: scan (threads) -> the batch assembled in the pinned
+// area (threads) -> the batch's chunks copied in, decoded and copied out on the device while the
+// threads apply the blocks whose strings are back (a thread waits for chunk j's results only when
+// it reaches a block with a string in it), so the device time hides under the apply pass.
 extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const uint8_t* blocks,
                                       const uint32_t* block_off, uint32_t nblocks, hpk_blocks_out* out) {
     if (!decs || !block_off || !out || (nblocks && block_off[nblocks] && !blocks)) return HPK_E_INVAL;
@@ -427,19 +627,10 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
     // at the end (a block's headers stay contiguous; blocks need not be in order in the arrays).
     int nth = (int)std::thread::hardware_concurrency();
     if (const char* e = getenv("HPK_HDEC_THREADS")) nth = atoi(e);  // (for measurements)
-    if (nth > 16) nth = 16;
+    if (nth > Pool::kMax) nth = Pool::kMax;
     if (nth < 1) nth = 1;
     if ((uint32_t)nth > nblocks / 256u + 1u) nth = (int)(nblocks / 256u + 1u);
-    auto parallel = [&](auto fn) {  // fn(thread index)
-        if (nth == 1) {
-            fn(0);
-            return;
-        }
-        std::vector<std::thread> th;
-        for (int t = 1; t < nth; ++t) th.emplace_back(fn, t);
-        fn(0);
-        for (auto& x : th) x.join();
-    };
+    auto parallel = [&](const std::function<void(int)>& fn) { pool().run(nth, fn); };
     static const bool timing = getenv("HPK_HDEC_TIMING") != nullptr;  // per-pass wall times to stderr
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t_0 = now();
@@ -458,6 +649,8 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
         thlen.resize(nth);
         W.outs.resize(nth);
     }
+    W.tin.assign(nth, 0);
+    W.tout.assign(nth, 0);
     auto blk0 = [&](int t) { return (uint32_t)((uint64_t)nblocks * t / nth); };
     parallel([&](int t) {
         // the vectors are moved into locals while the thread appends: their headers sit next to
@@ -473,33 +666,33 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
         hl.reserve(bytes / 8 + 16);
         for (uint32_t b = blk0(t); b < blk0(t + 1); ++b)
             scan_block(blocks, block_off[b], block_off[b + 1], (uint32_t)t, &pool, &scans[b], &ho, &hl);
+        uint64_t ti = 0, to = 0;  // the thread's string bytes and their decoded bounds
+        for (uint32_t x : hl) {
+            ti += x;
+            to += (hpk_decoded_bound(x) + 3) & ~(uint64_t)3;
+        }
+        W.tin[t] = ti;
+        W.tout[t] = to;
         pools[t] = std::move(pool);
         thoff[t] = std::move(ho);
         thlen[t] = std::move(hl);
     });
     std::vector<uint32_t>& lbase = W.lbase;  // each thread's first index in the batch
     lbase.assign(nth + 1, 0);
-    for (int t = 0; t < nth; ++t) lbase[t + 1] = lbase[t] + (uint32_t)thoff[t].size();
-    parallel([&](int t) {  // local Huffman indices -> batch indices
-        if (!lbase[t]) return;
-        for (Field& f : pools[t]) {
-            if (f.name.huff) f.name.lit += lbase[t];
-            if (f.value.huff) f.value.lit += lbase[t];
-        }
-    });
+    std::vector<uint64_t> ibase(nth + 1, 0), obase(nth + 1, 0);
+    for (int t = 0; t < nth; ++t) {
+        lbase[t + 1] = lbase[t] + (uint32_t)thoff[t].size();
+        ibase[t + 1] = ibase[t] + W.tin[t];
+        obase[t + 1] = obase[t] + W.tout[t];
+    }
     const long us_scan = us(t_0);
     auto t_1 = now();
     // pass 2: one batch for all of them. With a device context the batch is staged in the context's
     // page-locked host area (hpk_ctx_pinned), so its copies are DMA transfers that overlap the kernel
     // chunk by chunk; pageable vectors made HIP bounce every byte through its own staging buffer.
     const uint32_t n = lbase[nth];
-    size_t tot = 0, otot = 0;
-    for (int t = 0; t < nth; ++t)
-        for (size_t j = 0; j < thlen[t].size(); ++j) {
-            tot += thlen[t][j];
-            otot += ((hpk_decoded_bound(thlen[t][j]) + 3) & ~(size_t)3);
-            if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
-        }
+    const size_t tot = ibase[nth], otot = obase[nth];
+    if (tot >= (1ull << 32) || otot >= (1ull << 32)) return HPK_E_INVAL;
     uint8_t *in, *dec, *st;
     uint32_t *in_off, *out_off, *len;
     const size_t in_b = (tot + 16 + 15) & ~(size_t)15, dec_b = (otot + 16 + 15) & ~(size_t)15;
@@ -527,53 +720,95 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
         len = W.len.data();
         st = W.st.data();
     }
-    tot = 0;
-    otot = 0;
-    for (int t = 0; t < nth; ++t)
-        for (size_t j = 0; j < thlen[t].size(); ++j) {
-            const uint32_t i = lbase[t] + (uint32_t)j;
-            in_off[i] = (uint32_t)tot;
-            out_off[i] = (uint32_t)otot;
-            tot += thlen[t][j];
-            otot += ((hpk_decoded_bound(thlen[t][j]) + 3) & ~(size_t)3);
+    parallel([&](int t) {  // each thread's strings: offsets from its bases, bytes gathered
+        uint64_t io = ibase[t], oo = obase[t];
+        const uint32_t* ho = thoff[t].data();
+        const uint32_t* hl = thlen[t].data();
+        uint32_t* ino = in_off + lbase[t];
+        uint32_t* ouo = out_off + lbase[t];
+        for (size_t j = 0, m = thlen[t].size(); j < m; ++j) {
+            ino[j] = (uint32_t)io;
+            ouo[j] = (uint32_t)oo;
+            memcpy(in + io, blocks + ho[j], hl[j]);
+            io += hl[j];
+            oo += (hpk_decoded_bound(hl[j]) + 3) & ~(uint64_t)3;
         }
+    });
     in_off[n] = (uint32_t)tot;
     out_off[n] = (uint32_t)otot;
-    parallel([&](int t) {
-        for (size_t j = 0; j < thoff[t].size(); ++j)
-            memcpy(in + in_off[lbase[t] + j], blocks + thoff[t][j], thlen[t][j]);
-    });
+    int chunks = 0;
+    std::vector<uint32_t> cut(ctx ? hpk_ctx_max_chunks() + 1 : 1, 0);
     if (n) {
-        const int rc = ctx ? hpk_decode_batch(ctx, in, in_b, in_off, n, dec, dec_b, out_off, len, st, HPK_PTR_HOST)
+        const int rc = ctx ? hpk_decode_host_begin(ctx, in, in_b, in_off, n, dec, dec_b, out_off, len, st, &chunks,
+                                                   cut.data())
                            : hpk_decode_batch_cpu(in, in_off, n, dec, out_off, len, st, 0);
-        if (rc) return rc;
+        if (rc) {
+            if (ctx && chunks) (void)hpk_decode_host_end(ctx);
+            return rc;
+        }
     }
     const long us_batch = us(t_1);
     auto t_2 = now();
     // pass 3: apply; thread of a decoder = a hash of its address, its blocks in list order
     std::vector<Out>& outs = W.outs;
-    for (int t = 0; t < nth; ++t) {  // decoded headers take a few times the block bytes
-        outs[t].arena.clear();
-        outs[t].headers.clear();
-        outs[t].arena.reserve(4 * (size_t)block_off[nblocks] / (size_t)nth + 4096);
-        outs[t].headers.reserve(pools[t].size() + 16);
-    }
+    for (int t = 0; t < nth; ++t)  // decoded headers take a few times the block bytes
+        outs[t].reset(4 * (size_t)block_off[nblocks] / (size_t)nth + 4096, pools[t].size() + 16);
     // results go straight into the caller's malloc'd buffers (hpk_blocks_out_free)
     out->n_blocks = nblocks;
-    out->blocks = (hpk_block_result*)malloc((nblocks ? nblocks : 1) * sizeof(hpk_block_result));
-    if (!out->blocks) return HPK_E_INVAL;
+    out->blocks = (hpk_block_result*)g_out_cache.take(2, (size_t)nblocks * sizeof(hpk_block_result));
+    if (!out->blocks) {
+        if (chunks) (void)hpk_decode_host_end(ctx);
+        return HPK_E_INVAL;
+    }
     hpk_block_result* res = out->blocks;
     std::vector<uint8_t>& owner = W.owner;
     owner.resize(nblocks);
     for (uint32_t b = 0; b < nblocks; ++b)
         owner[b] = (uint8_t)(((uintptr_t)decs[b] >> 4) * 0x9E3779B97F4A7C15ull >> 59) % (uint32_t)nth;
-    const Huff h{dec, out_off, len, st};
+    const Huff h{dec, out_off, len, st, lbase.data()};
+    std::vector<int> wait_rc(nth, 0);
     parallel([&](int t) {
         Out mine = std::move(outs[t]);  // (a local: no false sharing with the neighbours' headers)
+        // this thread's blocks, in order; a block's fields and its Huffman strings are fetched a few
+        // blocks ahead (a thread's blocks are scattered over the batch: every string would otherwise
+        // be a cache miss on the critical path)
+        std::vector<uint32_t> my;
+        my.reserve(nblocks / nth + 64);
         for (uint32_t b = 0; b < nblocks; ++b)
-            if (owner[b] == t) apply_block(decs[b], blocks, scans[b], pools, h, mine, &res[b]);
+            if (owner[b] == t) my.push_back(b);
+        auto fetch_fields = [&](uint32_t b) {
+            const Field* f = pools[scans[b].pool].data() + scans[b].first;
+            for (uint32_t k = 0; k < scans[b].n; k += 1) __builtin_prefetch(f + k);
+        };
+        auto fetch_strings = [&](uint32_t b) {
+            const Field* f = pools[scans[b].pool].data() + scans[b].first;
+            const uint32_t lb = lbase[scans[b].pool];
+            for (uint32_t k = 0; k < scans[b].n; ++k) {
+                if (f[k].name.huff) __builtin_prefetch(dec + out_off[lb + f[k].name.lit]);
+                if (f[k].value.huff) __builtin_prefetch(dec + out_off[lb + f[k].value.lit]);
+            }
+        };
+        int waited = 0;  // device chunks whose results this thread has waited for
+        for (size_t i = 0; i < my.size() && !wait_rc[t]; ++i) {
+            const uint32_t b = my[i];
+            if (i + 4 < my.size()) fetch_fields(my[i + 4]);
+            if (i + 2 < my.size()) fetch_strings(my[i + 2]);
+            const uint32_t lit_end = lbase[scans[b].pool] + scans[b].lit_end;  // the block's strings end
+            while (waited < chunks && cut[waited] < lit_end)
+                if ((wait_rc[t] = hpk_host_chunk_wait(ctx, waited++))) break;
+            if (!wait_rc[t]) apply_block(decs[b], blocks, scans[b], pools, h, mine, &res[b]);
+        }
         outs[t] = std::move(mine);
     });
+    int rc = chunks ? hpk_decode_host_end(ctx) : HPK_E_OK;
+    for (int t = 0; t < nth && !rc; ++t) rc = wait_rc[t];
+    if (rc) {  // a device failure: the decoders are left as far as the apply pass got
+        g_out_cache.give(2, out->blocks, (size_t)nblocks * sizeof(hpk_block_result));
+        memset(out, 0, sizeof *out);
+        return rc;
+    }
+    const long us_apply = us(t_2);
+    auto t_3 = now();
     // join the per-thread outputs into the caller's buffers
     std::vector<uint32_t>&abase = W.abase, &hbase = W.hbase;
     abase.assign(nth, 0);
@@ -582,20 +817,20 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
     for (int t = 0; t < nth; ++t) {
         abase[t] = (uint32_t)at;
         hbase[t] = (uint32_t)ht;
-        at += outs[t].arena.size();
-        ht += outs[t].headers.size();
+        at += outs[t].an;
+        ht += outs[t].hn;
     }
     out->arena_len = at;
     out->n_headers = ht;
-    out->arena = (uint8_t*)malloc(at ? at : 1);
-    out->headers = (hpk_header*)malloc((ht ? ht : 1) * sizeof(hpk_header));
+    out->arena = (uint8_t*)g_out_cache.take(0, at);
+    out->headers = (hpk_header*)g_out_cache.take(1, ht * sizeof(hpk_header));
     if (at >= (1ull << 32) || !out->arena || !out->headers) {
         hpk_blocks_out_free(out);
         return HPK_E_INVAL;
     }
     parallel([&](int t) {
-        if (!outs[t].arena.empty()) memcpy(out->arena + abase[t], outs[t].arena.data(), outs[t].arena.size());
-        for (size_t j = 0; j < outs[t].headers.size(); ++j) {
+        if (outs[t].an) memcpy(out->arena + abase[t], outs[t].arena.data(), outs[t].an);
+        for (size_t j = 0; j < outs[t].hn; ++j) {
             hpk_header hd = outs[t].headers[j];
             hd.name_off += abase[t];
             hd.value_off += abase[t];
@@ -604,16 +839,16 @@ extern "C" int hpk_hdec_decode_blocks(hpk_ctx* ctx, hpk_hdec* const* decs, const
     });
     for (uint32_t b = 0; b < nblocks; ++b) res[b].first_header += hbase[owner[b]];
     if (timing)
-        fprintf(stderr, "hpk_hdec_decode_blocks: %d threads, scan %ld us, batch %ld us, apply+join %ld us\n", nth,
-                us_scan, us_batch, us(t_2));
+        fprintf(stderr, "hpk_hdec_decode_blocks: %d threads, scan %ld us, batch %s %ld us, apply %ld us, join %ld us\n",
+                nth, us_scan, ctx ? "issue" : "cpu", us_batch, us_apply, us(t_3));
     return HPK_E_OK;
 }
 
 extern "C" void hpk_blocks_out_free(hpk_blocks_out* out) {
     if (!out) return;
-    free(out->arena);
-    free(out->headers);
-    free(out->blocks);
+    g_out_cache.give(0, out->arena, out->arena_len);
+    g_out_cache.give(1, out->headers, out->n_headers * sizeof(hpk_header));
+    g_out_cache.give(2, out->blocks, (size_t)out->n_blocks * sizeof(hpk_block_result));
     memset(out, 0, sizeof *out);
 }
 
