@@ -75,6 +75,11 @@ __device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t gb
 // Keep a value's register live (and unchanged) up to here.
 __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 
+#ifndef HPK_LONG_PARK
+#define HPK_LONG_PARK 0  // long-code window: 0 three ring re-reads after the lookup; 1 a select from d3 or
+                         // one dword read beside the lookup (config 3 832-836 vs 817-822 us, r3s: 0 stays)
+#endif
+
 #ifndef HPK_LONG_OS
 #define HPK_LONG_OS 80  // output buffer bytes per lane (a multiple of 16; 80: 20-dword stride, 4-way bank aliasing instead of 96's 8-way, config 3 870 vs 883 us)
 #endif
@@ -302,7 +307,8 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 dg[4] += (unsigned long long)__popcll(__ballot(!(act && live && !done)));
             }
             if (!go) continue;
-            const uint32_t d3 = ring[(((X >> 5) + 2u) & (kRing - 1u)) * kBlock];
+            const uint32_t j0 = X >> 5;
+            const uint32_t d3 = ring[((j0 + 2u) & (kRing - 1u)) * kBlock];
             const uint32_t w = __builtin_amdgcn_alignbit(d0, d1, ~X);
             const uint32_t rem = Eb - X;
             const uint32_t e1 = s_lut[w >> (32 - HPK_LUT_BITS)];
@@ -345,6 +351,8 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             bool prog = a1 | park;
             if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup
                 const uint32_t wp = __builtin_amdgcn_alignbit(d0, d1, ~X);
+                const uint32_t d4 = HPK_LONG_PARK ? ring[((j0 + 3u) & (kRing - 1u)) * kBlock] : 0u;
+                const uint32_t dn = cross ? d4 : d3;  // the dword after d2
                 uint32_t sy, len;
                 bool eos;
                 lo_decode(wp, s_lo, sy, len, eos);
@@ -357,11 +365,19 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 } else {
                     obuf[ob - lb] = (uint8_t)sy;
                     ob += 1u;
-                    X += len;
-                    const uint32_t j = X >> 5;
-                    d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];
-                    d1 = ring[(j & (kRing - 1u)) * kBlock];
-                    d2 = ring[((j + 1u) & (kRing - 1u)) * kBlock];
+                    const uint32_t xp = X + len;  // (len <= 30: crosses at most one dword)
+                    if (HPK_LONG_PARK) {
+                        const bool c2 = (xp ^ X) > 31u;
+                        d0 = c2 ? d1 : d0;
+                        d1 = c2 ? d2 : d1;
+                        d2 = c2 ? dn : d2;
+                    } else {
+                        const uint32_t j = xp >> 5;
+                        d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];
+                        d1 = ring[(j & (kRing - 1u)) * kBlock];
+                        d2 = ring[((j + 1u) & (kRing - 1u)) * kBlock];
+                    }
+                    X = xp;
                 }
             }
             done = !prog;  // the literal has ended: finished at the next refill point
