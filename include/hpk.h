@@ -177,7 +177,11 @@ void hpk_arena_destroy(hpk_arena* arena);
  * `ctx` on the GPU, or, when ctx is NULL, by the library's CPU batch path
  * (hpk_decode_batch_cpu). Per block the result equals Decoder::decode_with_cb on the same state:
  * the headers emitted before the first error, and that error with the reference's precedence
- * (decoder.rs:368-450). Results are returned in library-allocated buffers (hpk_blocks_out_free). */
+ * (decoder.rs:368-450). Results are returned in library-allocated buffers (hpk_blocks_out_free,
+ * which keeps the largest freed buffers for the next call instead of returning them to the
+ * allocator). With a context the device batch runs while the blocks whose strings are back are
+ * applied: a device failure (HPK_E_DEVICE) mid-call leaves the decoders as far as the apply got,
+ * and `out` empty. Host threads: up to 16, HPK_HDEC_THREADS overrides (measurements). */
 typedef struct hpk_hdec hpk_hdec;
 
 typedef enum hpk_block_error {   /* DecoderError (decoder.rs:237-253) and its nested kinds */
