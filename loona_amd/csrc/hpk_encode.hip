@@ -141,6 +141,10 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
     }
 }
 
+#ifndef HPK_ENC_ORFULL
+#define HPK_ENC_ORFULL 0  // 1: pass 2 ORs a dword into the image once it is complete (and at a run's end),
+                          // not after every code
+#endif
 #ifndef HPK_ENC_PAIR
 #define HPK_ENC_PAIR 0  // 1: pass 2 ORs two codes at once where the whole wave can (measured slower)
 #endif
@@ -418,8 +422,8 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
                 auto put = [&](uint2 cl) {
                     acc = (acc << cl.y) | cl.x;
                     n += cl.y;  // 5 <= n < 62
-                    atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
                     const bool full = n >= 32u;
+                    if (!HPK_ENC_ORFULL || full) atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
                     dq += full ? 1u : 0u;
                     n &= 31u;
                 };

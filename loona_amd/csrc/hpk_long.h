@@ -80,6 +80,11 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
                          // one dword read beside the lookup (config 3 832-836 vs 817-822 us, r3s: 0 stays)
 #endif
 
+#ifndef HPK_LONG_PRIO
+#define HPK_LONG_PRIO 0  // > 0: a wave with a lane that has more than this many bits left runs at a higher
+                         // issue priority (s_setprio), so the phase's critical path issues first
+#endif
+
 #ifndef HPK_LONG_OS
 #define HPK_LONG_OS 80  // output buffer bytes per lane (a multiple of 16; 80: 20-dword stride, 4-way bank aliasing instead of 96's 8-way, config 3 870 vs 883 us)
 #endif
@@ -283,6 +288,12 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             dtp = t;
         }
         if (!__any(act)) break;  // no literal left for this wave
+        if (HPK_LONG_PRIO > 0) {
+            if (__any(act && Eb - X > (uint32_t)HPK_LONG_PRIO))
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
         // 6. the next two chunks, while the ring has room for them past the window's first dword
         if (act && h * 4u < span && h + 8u + 1u <= kRing + (X >> 5)) {
             P0 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u, 0, 0);

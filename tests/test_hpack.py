@@ -176,3 +176,44 @@ def test_every_truncation_of_rfc_blocks():
     assert sum(isinstance(x, hpack.DecoderError) for x in want) > 50
     for i, (gg, ww) in enumerate(zip(got, want)):
         assert gg == ww, (i, pairs[i][1].hex())
+
+
+def test_dynamic_table_churn_matches_restatement():
+    """Long runs of insertions, lookups, evictions and size updates through one decoder per stream,
+    all blocks in one call: the table's entry ring grows past its first 64 slots and its byte buffer
+    is compacted many times (hpk_hdec's allocation-free table); every block's headers or first error
+    equal decoder.rs's restatement (oracle/hpack_ref.py)."""
+    rng = random.Random(4096)
+    pairs, want = [], []
+    for stream in range(6):
+        d, r = hpack.Decoder(), hpack_ref.Decoder()
+        entries = 0
+        for _ in range(120):
+            blk = bytearray()
+            if rng.random() < 0.15:  # dynamic table size update (decoder.rs:538-554)
+                blk += hpack_ref.encode_integer(rng.choice([0, 100, 4096, 20000, 60000]), 5, 0x20)
+            for _ in range(rng.randrange(1, 24)):
+                op = rng.random()
+                if op < 0.55:  # literal with incremental indexing, new name
+                    nl = rng.choice([0, 1, 5, 12, 40, rng.randrange(0, 300)])
+                    vl = rng.choice([0, 3, 20, 100, rng.randrange(0, 5000)])
+                    blk += b"\x40" + hpack_ref.encode_integer(nl, 7, 0) + bytes(rng.randrange(97, 123) for _ in range(nl))
+                    blk += hpack_ref.encode_integer(vl, 7, 0) + bytes(rng.randrange(32, 127) for _ in range(vl))
+                    entries += 1
+                elif op < 0.75:  # literal with incremental indexing, indexed name
+                    idx = rng.randrange(1, 62) if rng.random() < 0.7 else rng.randrange(62, 65)
+                    vl = rng.randrange(0, 60)
+                    blk += hpack_ref.encode_integer(idx, 6, 0x40)
+                    blk += hpack_ref.encode_integer(vl, 7, 0) + bytes(rng.randrange(32, 127) for _ in range(vl))
+                    entries += 1
+                else:  # indexed field, sometimes past the table
+                    hi = 62 + min(entries, 400) + 3 if rng.random() < 0.05 else 65
+                    blk += hpack_ref.encode_integer(rng.randrange(1, hi), 7, 0x80)
+            w = bytes(blk)
+            pairs.append((d, w))
+            want.append(_ref_decode(r, w))
+    got = hpack.decode_blocks(pairs)
+    assert sum(isinstance(x, hpack.DecoderError) for x in want) > 10
+    assert sum(not isinstance(x, hpack.DecoderError) for x in want) > 300
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, pairs[i][1][:64].hex())
