@@ -781,10 +781,16 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         lds_barrier();
         if (tid == 0) s_ctr[5] = 0;  // its claim counter
         __syncthreads();  // (every thread's list entries and stores are out)
-        static_assert(kW + kO >= 512 * (32 * 4 + HPK_LONG_OS) && G::kInOff % 16 == 0 && kW % 16 == 0, "long-phase LDS");
-        long_phase<512, 8, 32, kMode == 5 ? 1 : 0, G::kBlock>(a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5],
-                                                              reinterpret_cast<uint32_t*>(s_in), s_in + 512 * 32 * 4,
-                                                              reinterpret_cast<uint4*>(s_q), s_lut, s_lo);
+        // rings, then output buffers, then the wave queues, over the window, image, fill queue and
+        // lengths (all free once the fills are done)
+        constexpr int kLB = HPK_LONG_WAVES * 64;
+        constexpr int kLQ = kLB * (HPK_LONG_RING * 4 + HPK_LONG_OS);
+        static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
+                          kW % 16 == 0 && kLQ % 16 == 0 && G::kHistOff == G::kInOff + kW + kO + 12 * kQ,
+                      "long-phase LDS");
+        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM>(
+            a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + kLB * HPK_LONG_RING * 4,
+            reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo);
     }
 }
 

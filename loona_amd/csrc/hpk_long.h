@@ -85,6 +85,19 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
                          // issue priority (s_setprio), so the phase's critical path issues first
 #endif
 
+#ifndef HPK_LONG_WAVES
+#define HPK_LONG_WAVES 8  // waves of the fill kernel's workgroup that run the phase (the others exit)
+#endif
+#ifndef HPK_LONG_U
+#define HPK_LONG_U 8  // steps between refill points
+#endif
+#ifndef HPK_LONG_CLAIM
+#define HPK_LONG_CLAIM 64  // list entries per claim (32 or 64)
+#endif
+#ifndef HPK_LONG_RING
+#define HPK_LONG_RING 32  // input ring dwords per lane
+#endif
+
 #ifndef HPK_LONG_OS
 #define HPK_LONG_OS 80  // output buffer bytes per lane (a multiple of 16; 80: 20-dword stride, 4-way bank aliasing instead of 96's 8-way, config 3 870 vs 883 us)
 #endif
@@ -94,17 +107,20 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 // s_q), kU steps between refill points, kRing input dwords per lane in s_ring and a kOS-byte
 // output buffer per lane in s_out (16-byte aligned). kDiag (diagnostic builds): per-wave counters
 // into a.dbg[wave * 16 + i] (scripts/diag_decode.py).
-template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll>
+template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64>
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
                                            const uint32_t* s_lut, const uint16_t* s_lo) {
-    constexpr uint32_t kChunk = 64;            // list entries per claim (one per lane)
-    constexpr uint32_t kQ = 2 * kChunk;        // per-wave queue: < 64 left + one claim
+    constexpr uint32_t kChunk = kClaim;        // list entries per claim (at most one per lane)
+    constexpr uint32_t kQ = kChunk;            // per-wave queue: a claim is made only once the lanes that
+                                               // want a literal have emptied the queue, so it never holds
+                                               // more than one claim
+    static_assert(kClaim == 32 || kClaim == 64, "claim size");
     // Output buffer per lane: bytes [lb, ob) of the output (lb 16-byte aligned) at [0, ob - lb). A
     // refill point stores every whole 16-byte group and moves the partial one (< 16 bytes) to the
     // front, so a period starts with <= 15 bytes and adds <= 5 per step: 15 + 5 kU + 3 bytes
     // (a step's 4-byte store) must fit.
-    constexpr uint32_t kOS = HPK_LONG_OS;
+    constexpr uint32_t kOS = kOSz;
     static_assert(15 + 5 * kU + 3 < (int)kOS, "output buffer");
     static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
     static_assert(kBlock % 64 == 0 && kBlock <= kBlockAll, "decoding waves");
@@ -269,7 +285,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             }
             // entries r + lane: [0, c1) from the front of the range, then from the back
             const uint32_t e = r + lane;
-            const bool ok = e < total;
+            const bool ok = lane < kChunk && e < total;
             const uint32_t lpos = ok ? (e < c1 ? ba + e : bb - 1u - (e - c1)) : ba;
             const uint32_t i0 = a.long_list[lpos];  // (a load either way: see the note below)
             const uint32_t i = ok ? i0 : 0u;

@@ -520,9 +520,10 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     if (c1 + c2) {
         static_assert(G::kWaveOff % 16 == 0, "long-phase rings");
         uint8_t* const area = smem + G::kWaveOff;
-        long_phase<512, 8, 32, 0, G::kBlock>(a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area),
-                                            area + 512 * 32 * 4,
-                                            reinterpret_cast<uint4*>(area + 512 * (32 * 4 + HPK_LONG_OS)), s_lut, s_lo);
+        constexpr int kLOS = 80;  // output buffer bytes per lane (the fill kernel's default geometry)
+        long_phase<512, 8, 32, 0, G::kBlock, kLOS>(a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area),
+                                                   area + 512 * 32 * 4,
+                                                   reinterpret_cast<uint4*>(area + 512 * (32 * 4 + kLOS)), s_lut, s_lo);
     }
     stamp(10);
     if (kMode == 3) {
