@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.25 gfx950 decode v25 (batches >= 4M literals: wave fills, each wave with its own LDS window and image, chunks handed out by guided self-scheduling, longest-first queue by an LDS counting sort, no workgroup barriers between fills; smaller batches: v24 workgroup fills; both: alignbit lane step with two LUT2 lookups, unconditional byte stores, static snake; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
+#define HPK_VERSION "hpk 0.26 gfx950 decode v26 (batches >= 4M literals: wave fills, each wave with its own LDS window and image, one chunk at a time handed out by guided self-scheduling, lane walk addressed from the LDS base, longest-first queue by an LDS counting sort, no workgroup barriers between fills; smaller batches: v24 workgroup fills; both: alignbit lane step with two LUT2 lookups, unconditional byte stores, static snake; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
 
 static thread_local std::string t_last_error;
 

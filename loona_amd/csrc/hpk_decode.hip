@@ -54,7 +54,10 @@ constexpr int kWaveWin = 3072, kWaveImg = 5888;
 #ifndef HPK_WAVE_RANK
 #define HPK_WAVE_RANK 0  // longest-first order: 0 LDS counting sort (32 classes), 1/2 ballots (16/32 classes)
 #endif
-#define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, 224u, HPK_WAVE_GUIDED, HPK_WAVE_RANK>
+#ifndef HPK_WAVE_CHUNK
+#define HPK_WAVE_CHUNK 224u  // least literals per chunk claim
+#endif
+#define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, HPK_WAVE_CHUNK, HPK_WAVE_GUIDED, HPK_WAVE_RANK>
 #define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN>
 
 #ifdef HPK_DIAG

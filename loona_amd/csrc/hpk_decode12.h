@@ -119,7 +119,9 @@ __device__ __forceinline__ void lit12_load(Lit12& L, const uint32_t* __restrict_
 // going to the lane's dummy slot out8[dmy] (no exec-mask branch around each store); kChecked
 // (diagnostic mode 4) checks every store against the literal's capacity, kNoStore (mode 2) stores
 // nothing.
-template <int kStore>
+template <int kStore, bool kP1 = false>  // kP1: a lookup's second byte stored at (address) + 1 by the
+                                         // store's offset (the wave kernel; in the fill kernel's
+                                         // register budget the extra live dmy - 1 spills)
 __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                            const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8,
                                            uint32_t dmy = 0) {
@@ -135,7 +137,10 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
     if (kStore == kPred) {
         out8[a1 ? L.o : dmy] = (uint8_t)e1;
-        out8[a2 ? L.o + 1 : dmy] = (uint8_t)(e1 >> 16);
+        if (kP1)
+            (out8 + 1)[a2 ? L.o : dmy - 1u] = (uint8_t)(e1 >> 16);
+        else
+            out8[a2 ? L.o + 1 : dmy] = (uint8_t)(e1 >> 16);
     } else {
         if (a1) put8(out8, L.o, e1, L.oend, kStore);
         if (a2) put8(out8, L.o + 1, e1 >> 16, L.oend, kStore);
@@ -154,7 +159,10 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
         b2 &= cont;
         if (kStore == kPred) {
             out8[b1 ? L.o : dmy] = (uint8_t)e2;
-            out8[b2 ? L.o + 1 : dmy] = (uint8_t)(e2 >> 16);
+            if (kP1)
+                (out8 + 1)[b2 ? L.o : dmy - 1u] = (uint8_t)(e2 >> 16);
+            else
+                out8[b2 ? L.o + 1 : dmy] = (uint8_t)(e2 >> 16);
         } else {
             if (b1) put8(out8, L.o, e2, L.oend, kStore);
             if (b2) put8(out8, L.o + 1, e2 >> 16, L.oend, kStore);

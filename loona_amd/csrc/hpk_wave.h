@@ -34,6 +34,7 @@
 #pragma once
 #include "hpk_decode12.h"
 
+
 namespace hpkdec {
 
 template <int kWinB, int kImgB>
@@ -154,14 +155,22 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         uint8_t* const s_win = smem + G::kWaveOff + wv * G::kWaveBytes;
         uint8_t* const s_img = s_win + kWinB;
         const uint32_t* const win32 = reinterpret_cast<const uint32_t*>(s_win);
-        const uint32_t dmy = (uint32_t)G::kImg + lane * 4u;
+        // The lane walk addresses the window and the image from the LDS array's base (its bit and
+        // output positions carry the wave's offsets), so a step's window read and byte stores take
+        // their base as the instruction's offset instead of a VGPR add each (v26; config 5 924-933 us
+        // with the one-chunk claims below, against 988-1001 us for v25: profiles/r03/s2/
+        // ab_wave_late_abs_r2.jsonl; with lit12_step's + 1 store offsets a step's block went from 82
+        // to 73 VALU in the ISA, and the kernel's 8 B/lane of scratch is gone)
+        const uint32_t wbits = (uint32_t)(G::kWaveOff + wv * G::kWaveBytes) * 8u;
+        const uint32_t obase = (uint32_t)(G::kWaveOff + wv * G::kWaveBytes + kWinB);
+        const uint32_t* const wl32 = reinterpret_cast<const uint32_t*>(smem);
+        uint8_t* const ol8 = smem;
+        const uint32_t dmy = obase + (uint32_t)G::kImg + lane * 4u;
         // The workgroup's range is handed out in chunks, in order, to whichever wave asks next (an LDS
         // cursor): a static split left the waves the SIMDs' arbitration favours idle at the end while
         // the others finished (11 % of a wave's time). Chunks shrink as the range drains (guided
         // self-scheduling: 1/32 of what is left, at least kChunk literals), so early chunks hold many
-        // fills (a chunk's last fill is usually partial) and the last ones even the waves out. A wave
-        // holds its current chunk and has already claimed the next one, whose first offsets are loaded a
-        // fill ahead of their use.
+        // fills (a chunk's last fill is usually partial) and the last ones even the waves out.
         // (!kGuided: the wave's static 1/16 of the range, then nothing)
         bool given = false;
         auto claim = [&](uint32_t& ca, uint32_t& ce) {
@@ -200,18 +209,16 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
 #pragma unroll
             for (int r = 0; r < R; ++r) ch[r] = g16[min((base16 >> 4) + lane + 64u * r, last16)];
         };
-        uint32_t cur, ce, na, ne;
+        // A wave holds one chunk at a time and claims the next when its current one ends (its first
+        // offsets are then loaded under the fill's setup): claimed a chunk ahead, the range's last
+        // chunks were held by a few waves while the workgroup's others waited (5 % of a wave's time)
+        uint32_t cur, ce;
         claim(cur, ce);
-        claim(na, ne);
-        uint32_t gin = 0, gout = 0, ngin = 0, ngout = 0;
+        uint32_t gin = 0, gout = 0;
         if (cur < ce) {
             gin = a.in_off[cur] + a.in_mis;
             gout = a.out_off[cur] + a.out_mis;
             prefetch(cur, ce, gin & ~15u);
-        }
-        if (na < ne) {
-            ngin = a.in_off[na];
-            ngout = a.out_off[na];
         }
         // the previous fill, not yet written back: literals [pcur, pcur + pk), output [pG0, pG1), and
         // each lane's (up to) two results: length | status << 24 and the literal's index in the fill
@@ -283,15 +290,13 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     *a.err = 1u;
                     s_ctr[0] = 1u;
                 }
-                for (;;) {  // this chunk's rest, the claimed next one, then every chunk still unclaimed
+                for (;;) {  // this chunk's rest, then every chunk still unclaimed
                     for (uint32_t i = cur + lane; i < ce; i += 64u) {
                         a.out_len[i] = 0;
                         a.status[i] = (uint8_t)HPK_BAD_OFFSETS;
                     }
-                    if (na >= ne) break;
-                    cur = na;
-                    ce = ne;
-                    claim(na, ne);
+                    claim(cur, ce);
+                    if (cur >= ce) break;
                 }
                 break;
             }
@@ -317,15 +322,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     }
                 }
                 cur += 1;
-                if (cur == ce) {  // the next chunk
-                    cur = na;
-                    ce = ne;
-                    claim(na, ne);
-                    if (na < ne) {
-                        ngin = a.in_off[na];
-                        ngout = a.out_off[na];
-                    }
-                }
+                if (cur == ce) claim(cur, ce);  // the next chunk
                 if (cur < ce) {
                     gin = a.in_off[cur] + a.in_mis;
                     gout = a.out_off[cur] + a.out_mis;
@@ -342,14 +339,10 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             // where the next fill starts: right after this one, or at the next chunk
             uint32_t cur_n = cur + k, ce_n = ce, gin_n = gin_end, gout_n = gout_end;
             if (cur_n == ce) {
-                cur_n = na;
-                ce_n = ne;
-                gin_n = ngin + a.in_mis;
-                gout_n = ngout + a.out_mis;
-                claim(na, ne);
-                if (na < ne) {
-                    ngin = a.in_off[na];
-                    ngout = a.out_off[na];
+                claim(cur_n, ce_n);
+                if (cur_n < ce_n) {
+                    gin_n = a.in_off[cur_n] + a.in_mis;
+                    gout_n = a.out_off[cur_n] + a.out_mis;
                 }
             }
             // 2. the previous fill's write-back (its image is read out before this fill's queue lands there)
@@ -431,13 +424,13 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 T.idx = e.y & 0xFFFu;
                 const uint32_t nb = e.x >> 16;
                 const uint32_t o = (e.y >> 12) & 0x1FFFFu;
-                T.X = (e.x & 0xFFFFu) * 8u + 31u;
+                T.X = wbits + (e.x & 0xFFFFu) * 8u + 31u;
                 T.Eb = T.X + (T.act ? nb * 8u : 0u);
-                T.o = o;
-                T.o0 = o;
+                T.o = obase + o;
+                T.o0 = obase + o;
                 T.st = HPK_OK;
                 T.prog = false;
-                lit12_load(T, win32);
+                lit12_load(T, wl32);
             };
             load(L, e1, t1);
             load(N, e2, t2);
@@ -450,7 +443,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 for (;;) {
                     dg_add(9, 1u);
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) lit12_step<kStore>(L, win32, s_lut, s_lo, s_img, dmy);
+                    for (int s = 0; s < 2; ++s) lit12_step<kStore, true>(L, wl32, s_lut, s_lo, ol8, dmy);
                     const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
                     if (__any(fin)) {
                         const bool sw = fin & nv;
@@ -470,9 +463,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             stamp(6);
             // results: the first slot's from its saved end state, the second's from the walk
             {
-                const uint32_t Eb = (e1.x & 0xFFFFu) * 8u + 31u + (e1.x >> 16) * 8u;
-                const uint32_t st = sSt != HPK_OK ? sSt : residual_status(Eb - sX, win_at(win32, sX - 31u));
-                rv0 = (sO - ((e1.y >> 12) & 0x1FFFFu)) | (st << 24);
+                const uint32_t Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (e1.x >> 16) * 8u;
+                const uint32_t st = sSt != HPK_OK ? sSt : residual_status(Eb - sX, win_at(wl32, sX - 31u));
+                rv0 = (sO - obase - ((e1.y >> 12) & 0x1FFFFu)) | (st << 24);
                 ri0 = s1 ? e1.y & 0xFFFu : 0xFFFFFFFFu;
                 rv1 = (Lend - L.o0) | (lit12_status(L) << 24);
                 ri1 = L.act ? L.idx : 0xFFFFFFFFu;
