@@ -141,14 +141,6 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
     }
 }
 
-#ifndef HPK_ENC_ORFULL
-#define HPK_ENC_ORFULL 0  // 1: pass 2 ORs a dword into the image once it is complete (and at a run's end),
-                          // not after every code
-#endif
-#ifndef HPK_ENC_PAIR
-#define HPK_ENC_PAIR 0  // 1: pass 2 ORs two codes at once where the whole wave can (measured slower)
-#endif
-constexpr bool kPair = HPK_ENC_PAIR;
 
 template <int kEB, int kEO, int kEQ, int kEBytes = 32, int kProf = 0>  // kEBytes: input bytes per thread per tile (16 or 32)
 // (at least 4 waves per SIMD: two 512-thread workgroups per CU fit only under 128 VGPRs)
@@ -423,7 +415,7 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
                     acc = (acc << cl.y) | cl.x;
                     n += cl.y;  // 5 <= n < 62
                     const bool full = n >= 32u;
-                    if (!HPK_ENC_ORFULL || full) atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
+                    atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
                     dq += full ? 1u : 0u;
                     n &= 31u;
                 };
@@ -431,22 +423,12 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
                 for (int j = 0; j < 8; j += 2) {
                     const uint2 c0 = tb[j], c1 = tb[j + 1];
                     if ((bm8 >> j) & 1u) start(j);
-                    // v5: two codes per OR when no run starts at the second byte and the two codes fit
-                    // the dword's room (n < 32 before, < 64 after: at most one dword completes); the
-                    // test is wave-uniform, so a wave takes one path or the other, never both
-                    const bool one = ((bm8 >> (j + 1)) & 1u) | (c0.y + c1.y > 32u);
-                    if (!kPair || __any(one)) {
-                        put(c0);
-                        if ((bm8 >> (j + 1)) & 1u) start(j + 1);
-                        put(c1);
-                    } else {
-                        acc = (((acc << c0.y) | c0.x) << c1.y) | c1.x;
-                        n += c0.y + c1.y;
-                        atomicOr(&S.img[dq], (uint32_t)((acc << (64u - n)) >> 32));
-                        const bool full = n >= 32u;
-                        dq += full ? 1u : 0u;
-                        n &= 31u;
-                    }
+                    // (two codes per OR where a whole wave can — no run start at the second byte, the
+                    // two codes within the dword's room — measured slower: config 3 537 vs 503-509 us;
+                    // ORing only complete dwords too: 510-514 vs 502-504 us)
+                    put(c0);
+                    if ((bm8 >> (j + 1)) & 1u) start(j + 1);
+                    put(c1);
                 }
             }
             if (any && !ph) {

@@ -75,16 +75,6 @@ __device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t gb
 // Keep a value's register live (and unchanged) up to here.
 __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 
-#ifndef HPK_LONG_PARK
-#define HPK_LONG_PARK 0  // long-code window: 0 three ring re-reads after the lookup; 1 a select from d3 or
-                         // one dword read beside the lookup (config 3 832-836 vs 817-822 us, r3s: 0 stays)
-#endif
-
-#ifndef HPK_LONG_PRIO
-#define HPK_LONG_PRIO 0  // > 0: a wave with a lane that has more than this many bits left runs at a higher
-                         // issue priority (s_setprio), so the phase's critical path issues first
-#endif
-
 #ifndef HPK_LONG_WAVES
 #define HPK_LONG_WAVES 8  // waves of the fill kernel's workgroup that run the phase (the others exit)
 #endif
@@ -304,12 +294,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             dtp = t;
         }
         if (!__any(act)) break;  // no literal left for this wave
-        if (HPK_LONG_PRIO > 0) {
-            if (__any(act && Eb - X > (uint32_t)HPK_LONG_PRIO))
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(0);
-        }
         // 6. the next two chunks, while the ring has room for them past the window's first dword
         if (act && h * 4u < span && h + 8u + 1u <= kRing + (X >> 5)) {
             P0 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u, 0, 0);
@@ -317,17 +301,14 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             pend = true;
         }
         // ---- kU steps while the input ring holds what a step can reach: a step advances < 2 dwords
-        // (<= 24 bits of lookups + a <= 30-bit long code) and reads up to dword (X >> 5) + 3 ----
-#ifndef HPK_LONG_BUDGET
-#define HPK_LONG_BUDGET 1  // 0: the ring check in every step (config 3 1026.9 vs 936.7 us)
-#endif
+        // (<= 24 bits of lookups + a <= 30-bit long code) and reads up to dword (X >> 5) + 3; the
+        // lane's budget of steps is set here, not checked per step (config 3 936.7 vs 1026.9 us) ----
         const uint32_t x5 = X >> 5;
         const uint32_t budget = !(act && live) ? 0u
                                 : h * 4u >= span ? (uint32_t)kU
                                 : x5 + 4u <= h ? min((uint32_t)kU, ((h - x5 - 4u) >> 1) + 1u) : 0u;
         for (int s = 0; s < kU; ++s) {
-            const bool go = HPK_LONG_BUDGET ? (uint32_t)s < budget && !done
-                                            : act && live && !done && ((X >> 5) + 4u <= h || h * 4u >= span);
+            const bool go = (uint32_t)s < budget && !done;
             if (kDiag) {
                 dg[2] += (unsigned long long)__popcll(__ballot(go));
                 dg[3] += (unsigned long long)__popcll(__ballot(act && live && !done && !go));
@@ -351,22 +332,15 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
             b1 &= cont;
             b2 &= cont;
-            {  // the step's (up to 4) bytes as one unaligned dword store into the lane's own buffer
-               // (bytes past the ones decoded are overwritten later or never stored out)
+            {  // the step's (up to 4) bytes as byte stores into the lane's own buffer (bytes past the
+               // ones decoded are overwritten later or never stored out; one unaligned dword store
+               // instead: config 3 936.7 vs 889.7 us, gfx950 splits it)
                 const uint32_t g1 = (uint32_t)a1 + (uint32_t)a2, g2 = (uint32_t)b1 + (uint32_t)b2;
-#ifndef HPK_LONG_U32
-#define HPK_LONG_U32 0  // 1: one unaligned dword store per step (config 3 936.7 vs 889.7 us: gfx950 splits it)
-#endif
-                if (HPK_LONG_U32) {
-                    const uint32_t pk = lut12_bytes(e1, g1) | (lut12_bytes(e2, g2) << (8u * g1));
-                    __builtin_memcpy(obuf + (ob - lb), &pk, 4);
-                } else {  // (byte stores: bytes past the decoded ones land in the buffer, harmless)
-                    uint8_t* const p = obuf + (ob - lb);
-                    p[0] = (uint8_t)e1;
-                    p[1] = (uint8_t)(e1 >> 16);
-                    p[g1] = (uint8_t)e2;
-                    p[g1 + 1] = (uint8_t)(e2 >> 16);
-                }
+                uint8_t* const p = obuf + (ob - lb);
+                p[0] = (uint8_t)e1;
+                p[1] = (uint8_t)(e1 >> 16);
+                p[g1] = (uint8_t)e2;
+                p[g1 + 1] = (uint8_t)(e2 >> 16);
                 ob += g1 + g2;
             }
             const uint32_t xn = X + u1 + (cont ? u2 : 0u);
@@ -378,8 +352,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             bool prog = a1 | park;
             if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup
                 const uint32_t wp = __builtin_amdgcn_alignbit(d0, d1, ~X);
-                const uint32_t d4 = HPK_LONG_PARK ? ring[((j0 + 3u) & (kRing - 1u)) * kBlock] : 0u;
-                const uint32_t dn = cross ? d4 : d3;  // the dword after d2
                 uint32_t sy, len;
                 bool eos;
                 lo_decode(wp, s_lo, sy, len, eos);
@@ -393,17 +365,12 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                     obuf[ob - lb] = (uint8_t)sy;
                     ob += 1u;
                     const uint32_t xp = X + len;  // (len <= 30: crosses at most one dword)
-                    if (HPK_LONG_PARK) {
-                        const bool c2 = (xp ^ X) > 31u;
-                        d0 = c2 ? d1 : d0;
-                        d1 = c2 ? d2 : d1;
-                        d2 = c2 ? dn : d2;
-                    } else {
-                        const uint32_t j = xp >> 5;
-                        d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];
-                        d1 = ring[(j & (kRing - 1u)) * kBlock];
-                        d2 = ring[((j + 1u) & (kRing - 1u)) * kBlock];
-                    }
+                    // the window re-read from the ring (a select from d3 or a fourth dword read beside
+                    // the lookup instead: config 3 832-836 vs 817-822 us)
+                    const uint32_t j = xp >> 5;
+                    d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];
+                    d1 = ring[(j & (kRing - 1u)) * kBlock];
+                    d2 = ring[((j + 1u) & (kRing - 1u)) * kBlock];
                     X = xp;
                 }
             }
