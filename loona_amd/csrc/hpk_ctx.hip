@@ -78,7 +78,7 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
 // slot is reused without a wait). Completion events are recorded only once a second stream has used
 // the context (an event record per launch cost ~1 us of a ~23 us small call); from then on a slot
 // taken over by another stream, or grown, waits for its last launch.
-int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list, int* slot) {
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
     int j = -1;
     bool any = false;
     for (int k = 0; k < hpk_ctx::kLongSlots; ++k) {
@@ -105,7 +105,7 @@ int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list, int* slot) {
         c->long_stream[j] = c->stream;
     }
     if (c->long_multi && !c->long_ev[j]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[j], hipEventDisableTiming));
-    if (c->long_list_cap[j] < n || !c->long_list[j]) {  // grow: the old list may still be in use
+    if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
         if (c->long_ev_set[j])
             HIP_TRY(hipEventSynchronize(c->long_ev[j]));
         else if (c->long_list[j])
@@ -113,7 +113,7 @@ int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list, int* slot) {
         (void)hipFree(c->long_list[j]);
         c->long_list[j] = nullptr;
         c->long_list_cap[j] = 0;
-        const size_t cap = n + (n >> 3);  // (n: the words this launch needs)
+        const size_t cap = (size_t)n + (n >> 2) + 1024;
         HIP_TRY(hipMalloc(&c->long_list[j], cap * sizeof(uint32_t)));
         c->long_list_cap[j] = cap;
     }

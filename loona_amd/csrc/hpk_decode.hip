@@ -40,13 +40,6 @@ constexpr int kWaves = 16, kW = 40960, kO = 79104, kQ = 2048, kRefillN = 2;
 #ifndef HPK_LONG_BIG
 #define HPK_LONG_BIG 1024
 #endif
-// split long literals (HPK_SPLIT, hpk_long.h: two pieces, joined where their walks meet)
-#ifndef HPK_SPLIT_MIN
-#define HPK_SPLIT_MIN 1536
-#endif
-#ifndef HPK_SPLIT_MAX
-#define HPK_SPLIT_MAX 6144
-#endif
 using Geo = Geo12<kWaves, kW, kO, kQ>;
 // Wave-fill kernel (v25, hpk_wave.h): per wave a 3 KiB window and a 5.75 KiB image, the workgroup's
 // range handed out in chunks of 224 literals; for batches of at least HPK_WAVE_MIN literals (smaller
@@ -87,12 +80,6 @@ extern "C" int hpk_debug_stamps(unsigned long long* host, size_t cap_entries) {
 }
 #endif
 
-#if HPK_SPLIT_DIAG
-extern "C" int hpk_debug_split_stat(unsigned long long* host4) {
-    return hipMemcpyFromSymbol(host4, HIP_SYMBOL(g_split_stat), 4 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     DecodeArgs a;
     const uintptr_t ip = (uintptr_t)b.in_blob;
@@ -116,23 +103,13 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.err = c->d_err;
     uint32_t* ll = nullptr;
     int lslot = 0;
-    // the long list: n entries (a workgroup's literal range), then the split slots (a quarter of
-    // the range per workgroup) and, 16-byte aligned, two 16-byte records per split slot
-    const bool split = HPK_SPLIT && b.n < (1u << 23);
-    const size_t nlist = (size_t)b.n + (b.n >> 2) + 1024;
-    const size_t words = nlist + (split ? 4 + 8 * ((size_t)(b.n >> 2) + 1024) : 0);
-    if (int rc = hpk_long_list(c, words, &ll, &lslot)) return rc;
+    if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
     a.long_list = ll;
     a.long_min = HPK_LONG_MIN;
     a.long_big = HPK_LONG_BIG;
-    a.split_base = split ? b.n : 0u;
-    a.split_min = split ? HPK_SPLIT_MIN : 0xFFFFFFFFu;
-    a.split_max = HPK_SPLIT_MAX;
-    a.split_rec = split ? reinterpret_cast<uint4*>(((uintptr_t)(ll + nlist) + 15) & ~(uintptr_t)15) : nullptr;
 #ifdef HPK_DIAG
     if (const char* lm = getenv("HPK_LONG_MIN")) a.long_min = (uint32_t)atoi(lm);
     if (const char* lb = getenv("HPK_LONG_BIG")) a.long_big = (uint32_t)atoi(lb);
-    if (const char* sm = getenv("HPK_SPLIT_MIN")) a.split_min = split ? (uint32_t)atoi(sm) : 0xFFFFFFFFu;
 #endif
     // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;

@@ -359,28 +359,15 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     };
     // long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
-    // A literal of [split_min, split_max] bytes (kSplit) takes one of the workgroup's split slots
-    // long_list[split_base + BA / 4, split_base + BB / 4) (count in s_ctr[11]), which holds its index,
-    // and is listed as its piece A (bit 30 | slot); long_phase lists its piece B by the slot.
-    const uint32_t sq0 = BA >> 2, scap = (BB >> 2) - (BA >> 2);
     auto leave = [&](uint32_t i, uint32_t nb) {
-        uint32_t v = i;
-        if (HPK_SPLIT && nb >= a.split_min && nb <= a.split_max) {
-            const uint32_t k = atomicAdd(&s_ctr[11], 1u);
-            if (k < scap) {
-                a.long_list[a.split_base + sq0 + k] = i;
-                v = (1u << 30) | (sq0 + k);
-            }
-        }
         if (nb >= a.long_big)
-            a.long_list[BA + atomicAdd(&s_ctr[6], 1u)] = v;
+            a.long_list[BA + atomicAdd(&s_ctr[6], 1u)] = i;
         else
-            a.long_list[BB - 1u - atomicAdd(&s_ctr[7], 1u)] = v;
+            a.long_list[BB - 1u - atomicAdd(&s_ctr[7], 1u)] = i;
     };
     if (tid == 0) {
         s_ctr[6] = 0;
         s_ctr[7] = 0;
-        s_ctr[11] = 0;
         s_ctr[8] = 0;
         s_ctr[9] = 0;
     }
@@ -409,7 +396,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         // the long-list counts before this fill (nothing changes them until the setup below): a fill
         // found bad takes back what its own literals listed
-        const uint32_t lcnt6 = s_ctr[6], lcnt7 = s_ctr[7], lcnt11 = HPK_SPLIT ? s_ctr[11] : 0u;
+        const uint32_t lcnt6 = s_ctr[6], lcnt7 = s_ctr[7];
         if (tid < 64) s_hist[tid] = 0;
         if (tid == 0) {
             s_ctr[0] = 0;
@@ -495,7 +482,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 *a.err = 1u;
                 s_ctr[6] = lcnt6;  // this fill's long literals are void too: not for the long-literal phase
                 s_ctr[7] = lcnt7;
-                if (HPK_SPLIT) s_ctr[11] = lcnt11;
             }
             break;
         }
@@ -511,7 +497,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[6] = 0;  // (this fill's entries are listed again below)
                     s_ctr[7] = 0;
-                    s_ctr[11] = 0;
                     s_ctr[10] = 0;
                 }
                 lds_barrier();
@@ -535,7 +520,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[6] = 0;
                     s_ctr[7] = 0;
-                    s_ctr[11] = 0;
                 }
                 continue;  // this fill again, from its setup (its prefetched offsets and window are still
                            // in the registers)
@@ -812,16 +796,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
                           kW % 16 == 0 && kLQ % 16 == 0 && G::kHistOff == G::kInOff + kW + kO + 12 * kQ,
                       "long-phase LDS");
-        const uint32_t cs = HPK_SPLIT && a.split_base ? min(s_ctr[11], scap) : 0u;
-        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM,
-                   HPK_SPLIT != 0>(
+        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM>(
             a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + kLB * HPK_LONG_RING * 4,
-            reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo, cs, a.split_base + sq0);
-        if (HPK_SPLIT && cs && HPK_SPLIT_DIAG != 2) {  // (block-uniform) the split literals' joins, once every piece has ended
-            __syncthreads();
-            static_assert(G::kBlock * (16 + 48) <= kW + kO, "split join LDS");
-            split_join<G::kBlock>(a, a.split_base + sq0, cs, s_in, s_lo);
-        }
+            reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo);
     }
 }
 

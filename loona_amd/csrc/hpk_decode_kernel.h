@@ -37,12 +37,6 @@ struct DecodeArgs {
     // those of >= long_big bytes from the front, the others from the back
     uint32_t* long_list;
     uint32_t long_min, long_big;
-    // split long literals (fill kernel, batches below 2^23 literals; split_base 0 = off): a literal of
-    // [split_min, split_max] encoded bytes is decoded as two pieces by two lanes and joined
-    // (hpk_long.h): its slot k in long_list[split_base + ...) holds the literal index, records
-    // split_rec[2k] (piece A) and [2k + 1] (piece B)
-    uint4* split_rec;
-    uint32_t split_min, split_max, split_base;
 };
 
 // Per-lane state of the literal being decoded.

@@ -58,7 +58,7 @@ struct hpk_ctx {
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on
 // first use; HPK_E_OK or an error code); *slot is passed to hpk_long_list_used after the launch.
-int hpk_long_list(hpk_ctx* c, size_t n, uint32_t** list, int* slot);
+int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot);
 // Records the slot's event on the context's stream after the launch that reads the list.
 int hpk_long_list_used(hpk_ctx* c, int slot);
 

@@ -81,9 +81,6 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 #ifndef HPK_LONG_U
 #define HPK_LONG_U 8  // steps between refill points
 #endif
-#ifndef HPK_SPLIT
-#define HPK_SPLIT 0  // 1: the fill kernel splits literals of [split_min, split_max] bytes (split_join)
-#endif
 #ifndef HPK_LONG_CLAIM
 #define HPK_LONG_CLAIM 64  // list entries per claim (32 or 64)
 #endif
@@ -100,20 +97,10 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 // s_q), kU steps between refill points, kRing input dwords per lane in s_ring and a kOS-byte
 // output buffer per lane in s_out (16-byte aligned). kDiag (diagnostic builds): per-wave counters
 // into a.dbg[wave * 16 + i] (scripts/diag_decode.py).
-// kSplit: cs split literals of the workgroup have their slots at long_list[sb, sb + cs); each is
-// decoded as two pieces (split_join below): piece A, listed among the range's entries with bit 30
-// and its slot, is the literal's first m = nbytes / 2 bytes; piece B, listed by its slot between the
-// two classes, is the rest, decoding from byte m as if a code started there, its output at the
-// region's byte G = 8 m / 5 (the bound of A's bytes, so the two never overlap). A piece ends with a
-// record instead of a length and status.
-constexpr uint32_t kSyncBits = 2048;  // a split literal's B piece restarts after an EOS this close to
-                                      // its start or last restart (unsynchronised walks can read one)
-template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64,
-          bool kSplit = false>
+template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64>
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
-                                           const uint32_t* s_lut, const uint16_t* s_lo, uint32_t cs = 0,
-                                           uint32_t sb = 0) {
+                                           const uint32_t* s_lut, const uint16_t* s_lo) {
     constexpr uint32_t kChunk = kClaim;        // list entries per claim (at most one per lane)
     constexpr uint32_t kQ = kChunk;            // per-wave queue: a claim is made only once the lanes that
                                                // want a literal have emptied the queue, so it never holds
@@ -128,8 +115,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
     static_assert(kBlock % 64 == 0 && kBlock <= kBlockAll, "decoding waves");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    if (!kSplit) cs = 0;
-    const uint32_t total = c1 + cs + c2;
+    const uint32_t total = c1 + c2;
     if (total == 0) return;  // (block-uniform: nothing left to this phase)
     if (tid >= (uint32_t)kBlock) return;  // (no barrier follows)
     uint4 (*sq)[kQ] = reinterpret_cast<uint4 (*)[kQ]>(s_q);
@@ -139,7 +125,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     const __amdgpu_buffer_rsrc_t r_out = buf_rsrc(a.out_base, a.out_cap + a.out_mis);
     const __amdgpu_buffer_rsrc_t r_len = buf_rsrc(a.out_len, min(a.n, 0x3FFFFFFFu) * 4u);
     const __amdgpu_buffer_rsrc_t r_st = buf_rsrc(a.status, a.n);
-    const __amdgpu_buffer_rsrc_t r_rec = buf_rsrc(a.split_rec, kSplit && a.split_rec ? 0x7FFFFFF0u : 0u);
     uint32_t* ring = s_ring + tid;        // input dword j: ring[(j % kRing) * kBlock]
     uint8_t* const obuf = s_out + tid * kOS;  // output byte p: obuf[p - lb]
     bool more = true;               // wave-uniform: claims may remain
@@ -152,7 +137,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     bool act = false, live = false, pend = false, done = false;
     uint32_t idx = 0, X = 0, Eb = 0, d0 = 0, d1 = 0, d2 = 0, st = HPK_OK, q0 = 0, span = 0, h = 0;
     uint32_t o0 = 0, ob = 0, fl = 0, lb = 0;
-    uint32_t xs = 0, sR = 0, cR = 0;  // kSplit: the piece's first X, B's last (re)start X and its bytes then
     u32x4 P0 = {}, P1 = {};
     unsigned long long dg[10] = {};  // kDiag: 0 cycles, 1 points, 2 lane-steps, 3 stalled, 4 idle,
                                      // 5 assign cycles, 6 step cycles, 7 refill cycles, 8 literals
@@ -188,8 +172,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
         // to the buffer's front. Every register a store reads its data from stays live until after
         // the steps (pin).
         u32x4 gv[4];
-        uint32_t hv[4], hb[16], tv[4], tb[16], lv = 0, sv = 0, ra = 0;
-        u32x4 rcv = {};
+        uint32_t hv[4], hb[16], tv[4], tb[16], lv = 0, sv = 0;
         uint32_t ha = 0, ga = 0, ta = 0, ia = 0, ja = 0;  // their addresses (pinned too)
         {
             const uint32_t gb = fl & ~15u;  // (== lb: nothing of the literal is stored yet)
@@ -228,8 +211,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
         }
         // 4. a literal that ended in the last steps: padding check, last bytes, length, status
         if (done) {
-            if (st == HPK_OK && !(kSplit && (idx >> 30) == 1u))
-                st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
+            if (st == HPK_OK) st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
             if (ob > fl) {  // [fl, ob) lies in one group, at the buffer's front
                 const uint32_t gb = fl & ~15u;
                 ta = gb;
@@ -244,15 +226,8 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             sv = st;
             ia = idx * 4u;
             ja = idx;
-            if (!kSplit || (idx >> 30) == 0u) {
-                __builtin_amdgcn_raw_buffer_store_b32(lv, r_len, ia, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sv, r_st, ja, 0, 0);
-            } else {  // a piece: its record (A: bits, bytes, EOS or not; B: restart bits, bytes then, bytes, status)
-                const bool pb = (idx >> 30) == 2u;
-                rcv = pb ? u32x4{sR - xs, cR, lv, sv} : u32x4{X - xs, lv, sv == HPK_EOS_IN_STRING ? 1u : 0u, 0u};
-                ra = ((idx & 0x3FFFFFFFu) * 2u + (pb ? 1u : 0u)) * 16u;
-                __builtin_amdgcn_raw_buffer_store_b128(rcv, r_rec, ra, 0, 0);
-            }
+            __builtin_amdgcn_raw_buffer_store_b32(lv, r_len, ia, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sv, r_st, ja, 0, 0);
             act = false;
             live = false;
             done = false;
@@ -279,9 +254,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 span = p1 - (q0 << 4);  // bytes from the first chunk's start to the literal's end
                 X = (p0 & 15u) * 8u + 31u;
                 Eb = X + (p1 - p0) * 8u;
-                xs = X;
-                sR = X;
-                cR = 0;
                 h = 0;
                 st = HPK_OK;
                 o0 = e.w + a.out_mis;
@@ -301,30 +273,16 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 more = false;
                 break;
             }
-            // entries r + lane: [0, c1) from the front of the range, then (kSplit) the cs split
-            // slots' B pieces, then from the back
+            // entries r + lane: [0, c1) from the front of the range, then from the back
             const uint32_t e = r + lane;
             const bool ok = lane < kChunk && e < total;
-            const bool inB = kSplit && e >= c1 && e - c1 < cs;
-            const uint32_t lpos = ok ? (e < c1 ? ba + e : inB ? sb + (e - c1) : bb - 1u - (e - c1 - cs)) : ba;
+            const uint32_t lpos = ok ? (e < c1 ? ba + e : bb - 1u - (e - c1)) : ba;
             const uint32_t i0 = a.long_list[lpos];  // (a load either way: see the note below)
-            uint4 li;
-            if (!kSplit) {
-                const uint32_t i = ok ? i0 : 0u;
-                // straight-line loads (no branch around them): a load under a branch leaves the compiler
-                // unsure whether its register is still pending, and it then waits for all memory
-                // operations (the refill loads included) before the steps reuse the register
-                li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.out_off[i]);
-            } else {  // (the same, with the piece's slot resolved to its literal by one more load)
-                const bool isA = !inB && (i0 >> 30) == 1u;
-                const uint32_t ks = inB ? lpos - a.split_base : (i0 & 0x3FFFFFFFu);
-                const uint32_t i1 = a.long_list[isA ? a.split_base + ks : lpos];
-                const uint32_t i = ok ? (isA ? i1 : i0 & 0x3FFFFFFFu) : 0u;
-                const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q = a.out_off[i];
-                const uint32_t m = (p1 - p0) >> 1;
-                li = isA ? make_uint4((1u << 30) | ks, p0, p0 + m, q)
-                         : inB ? make_uint4((2u << 30) | ks, p0 + m, p1, q + (8u * m) / 5u) : make_uint4(i, p0, p1, q);
-            }
+            const uint32_t i = ok ? i0 : 0u;
+            // straight-line loads (no branch around them): a load under a branch leaves the compiler
+            // unsure whether its register is still pending, and it then waits for all memory
+            // operations (the refill loads included) before the steps reuse the register
+            const uint4 li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.out_off[i]);
             const uint64_t lm = __ballot(ok);
             const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
             if (ok) sq[wv][(qt + lr) % kQ] = li;
@@ -397,24 +355,15 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 uint32_t sy, len;
                 bool eos;
                 lo_decode(wp, s_lo, sy, len, eos);
-                // (kSplit: an EOS read by a B piece within kSyncBits of its (re)start is taken as a
-                // sign that its walk is not yet in step: it goes on after it, and the join starts
-                // its meeting walk for B from there)
-                const bool rs = kSplit && eos && (idx >> 30) == 2u && X - sR < kSyncBits;
                 if (len > Eb - X) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
                     st = HPK_PADDING_TOO_LARGE;
                     prog = false;
-                } else if (eos && !rs) {  // huffman.rs:112-116
+                } else if (eos) {  // huffman.rs:112-116
                     st = HPK_EOS_IN_STRING;
                     prog = false;
                 } else {
-                    if (!rs) {
-                        obuf[ob - lb] = (uint8_t)sy;
-                        ob += 1u;
-                    } else {
-                        sR = X + len;
-                        cR = ob - o0;
-                    }
+                    obuf[ob - lb] = (uint8_t)sy;
+                    ob += 1u;
                     const uint32_t xp = X + len;  // (len <= 30: crosses at most one dword)
                     // the window re-read from the ring (a select from d3 or a fourth dword read beside
                     // the lookup instead: config 3 832-836 vs 817-822 us)
@@ -445,13 +394,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
         }
         pin(lv);
         pin(sv);
-        if (kSplit) {
-            pin(rcv.x);
-            pin(rcv.y);
-            pin(rcv.z);
-            pin(rcv.w);
-            pin(ra);
-        }
         pin(ha);
         pin(ga);
         pin(ta);
@@ -467,168 +409,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             for (int i = 0; i < 10; ++i) v = lane == (uint32_t)i ? dg[i] : v;
             a.dbg[gw * 16u + lane] = v;
         }
-    }
-}
-
-
-// Split literals' join (kSplit), after the long-literal phase: every piece has ended and written its
-// record. Rounds of up to kBlockAll slots: (1) one thread per slot walks A's codes from where A
-// stopped and B's from its last (re)start, code by code from global memory, the one further behind
-// advancing, until both stand on the same bit (the stream's and B's code boundaries coincide from
-// there on: ~41 bits past the middle byte on config 3); A's codes walked meanwhile are the literal's
-// bytes between A's end and B's part, kept in LDS; (2) one wave per slot writes them, then moves B's
-// bytes from the meeting point on (B decoded them at region byte G) to follow, every load issued
-// before any store, 16 bytes per lane and round. The literal's length is A's bytes + the walked bytes
-// + B's bytes past the meeting point, its status B's (the literal's end is B's). A literal whose walk
-// reaches an EOS on A's side ends there (EOSInString, the bytes before it); one whose walks do not
-// meet (or whose B part would not fit the registers of the move) is decoded whole by one lane.
-#ifndef HPK_SPLIT_DIAG
-#define HPK_SPLIT_DIAG 0  // experiments: 1 no whole-literal decodes, 2 no join, 3 count them (g_split_stat)
-#endif
-#if HPK_SPLIT_DIAG
-__device__ unsigned long long g_split_stat[4];  // slots, walks failed, A EOS, walked bits
-#endif
-template <int kBlockAll>
-__device__ __forceinline__ void split_join(const DecodeArgs& a, uint32_t sb, uint32_t cs, uint8_t* s_area,
-                                        const uint16_t* s_lo) {
-    constexpr uint32_t kE = 48;        // walked bytes kept per slot
-    constexpr int kMR = 5;             // move rounds: up to 5 KiB of B's bytes (split_max <= 6144)
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    uint4* const jobs = reinterpret_cast<uint4*>(s_area);                  // kBlockAll x 16 B
-    uint8_t* const ebuf = s_area + kBlockAll * 16;                         // kBlockAll x kE
-    const uint32_t* const g32 = reinterpret_cast<const uint32_t*>(a.in_base);
-    const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
-    const uint32_t last_dw = in_end ? (in_end - 1u) >> 2 : 0u;
-    const __amdgpu_buffer_rsrc_t r_out = buf_rsrc(a.out_base, a.out_cap + a.out_mis);
-    // 32 bits of the stream at bit `pos` of the literal starting at byte `bo` (from in_base)
-    auto bits32 = [&](uint32_t bo, uint32_t pos) {
-        const uint32_t b = (bo & 3u) * 8u + pos;
-        const uint32_t j = (bo >> 2) + (b >> 5);
-        const uint64_t d = ((uint64_t)__builtin_bswap32(g32[min(j, last_dw)]) << 32) |
-                           __builtin_bswap32(g32[min(j + 1u, last_dw)]);
-        return (uint32_t)((d << (b & 31u)) >> 32);
-    };
-    for (uint32_t t0 = 0; t0 < cs; t0 += kBlockAll) {
-        const uint32_t nr = min(cs - t0, (uint32_t)kBlockAll);
-        // (1) the meeting walks
-        if (tid < nr) {
-            const uint32_t kk = sb + t0 + tid, ks = kk - a.split_base;
-            const uint32_t i = a.long_list[kk];
-            const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q = a.out_off[i];
-            const uint32_t nb = p1 - p0, m = nb >> 1, G = (8u * m) / 5u;
-            const uint4 rA = a.split_rec[2u * ks], rB = a.split_rec[2u * ks + 1u];
-            const uint32_t cA = rA.y;
-            uint4 job = make_uint4(i, 0u, 0u, 0u);  // x: i | e << 23 | kind << 30 (0 move, 1 none, 2 whole)
-            uint8_t* const eb = ebuf + tid * kE;
-            if (rA.z) {  // A read an EOS: huffman.rs:112-116, the bytes before it
-                a.out_len[i] = cA;
-                a.status[i] = (uint8_t)HPK_EOS_IN_STRING;
-                job.x = i | (1u << 30);
-            } else {
-                const uint32_t nbits = 8u * nb, bo = p0 + a.in_mis;
-                uint32_t pa = rA.x, pb = 8u * m + rB.x, cb = 0, e = 0;
-                bool fail = false, eos = false;
-                for (uint32_t it = 0; pa != pb; ++it) {
-                    const bool sa = pa < pb;
-                    const uint32_t pos = sa ? pa : pb;
-                    uint32_t sym, len;
-                    bool eo;
-                    lo_decode(bits32(bo, pos), s_lo, sym, len, eo);
-                    if (it >= 1024u || len > nbits - pos || (eo && !sa) || (sa && !eo && e >= kE)) {
-                        fail = true;
-                        break;
-                    }
-                    if (eo) {
-                        eos = true;
-                        break;
-                    }
-                    if (sa) {
-                        eb[e++] = (uint8_t)sym;
-                        pa += len;
-                    } else {
-                        pb += len;
-                        ++cb;
-                    }
-                }
-                const uint32_t kB = rB.y + cb, lenB = rB.z;
-                const uint32_t mv = eos ? 0u : lenB - kB;
-                if (!fail && !eos && (kB > lenB || mv > 1024u * kMR)) fail = true;
-#if HPK_SPLIT_DIAG
-                atomicAdd(&g_split_stat[0], 1ull);
-                if (fail) atomicAdd(&g_split_stat[1], 1ull);
-                atomicAdd(&g_split_stat[3], (unsigned long long)(pa - 8u * m));
-#endif
-                if (fail) {
-                    job.x = i | (2u << 30);
-                } else {
-                    a.out_len[i] = cA + e + mv;
-                    a.status[i] = (uint8_t)(eos ? HPK_EOS_IN_STRING : rB.w);
-                    job = make_uint4(i | (e << 23), q + G + kB + a.out_mis, q + cA + a.out_mis, mv);
-                }
-            }
-            jobs[tid] = job;
-        }
-        __syncthreads();
-        // (2) one wave per slot: the walked bytes, then B's bytes from the meeting point on
-        for (uint32_t j = wv; j < nr; j += kBlockAll / 64) {
-            const uint4 job = jobs[j];
-            const uint32_t kind = job.x >> 30, i = job.x & 0x7FFFFFu;
-            if (kind == 1u) continue;
-            if (kind == 2u) {  // one lane decodes the literal whole (lit_bytes_to: the byte path's semantics)
-                if (lane == 0 && HPK_SPLIT_DIAG != 1) {
-                    const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q = a.out_off[i];
-                    const GlobalSrc g{g32, last_dw};
-                    uint8_t* dst = a.out_base + q + a.out_mis;
-                    Lit L = {};
-                    lit_bytes_to(L, g, s_lo, [&](uint32_t k, uint8_t v) { dst[k] = v; }, a.out_off[i + 1] - q,
-                                 p0 + a.in_mis, p1 - p0);
-                    a.out_len[i] = L.cnt;
-                    a.status[i] = (uint8_t)lit_status(L);
-                }
-                continue;
-            }
-            const uint32_t e = (job.x >> 23) & 0x7Fu, src = job.y, D = job.z + e, n = job.w;
-            // B's bytes [src, src + n) to [D, D + n): whole 16-byte destination chunks by lanes, the
-            // head and tail (< 16 bytes each) bytewise; all loads first (the ranges may overlap)
-            const uint32_t c0 = (D + 15u) >> 4, c1 = (D + n) >> 4;  // whole chunks [c0, c1)
-            const uint32_t nch = c1 > c0 ? c1 - c0 : 0u;
-            const uint32_t hd = c1 > c0 ? (c0 << 4) - D : n;      // head bytes
-            const uint32_t tl = c1 > c0 ? D + n - (c1 << 4) : 0u; // tail bytes
-            uint32_t w[kMR][5];
-#pragma unroll
-            for (int r = 0; r < kMR; ++r) {
-                const uint32_t c = lane + 64u * (uint32_t)r;
-                const uint32_t s = src + ((c0 + min(c, nch ? nch - 1u : 0u)) << 4) - D;  // its first source byte
-#pragma unroll
-                for (int k = 0; k < 5; ++k)
-                    w[r][k] = __builtin_amdgcn_raw_buffer_load_b32(r_out, ((s >> 2) + (uint32_t)k) * 4u, 0, 1);
-            }
-            // head / tail bytes: lanes 0..hd-1 the head, 16..16+tl-1 the tail
-            const bool hb = lane < hd, tb = lane >= 16u && lane - 16u < tl;
-            const uint32_t bx = hb ? lane : tb ? hd + 16u * nch + (lane - 16u) : 0u;  // byte index in B's part
-            const uint32_t bv = __builtin_amdgcn_raw_buffer_load_b8(r_out, src + bx, 0, 1);
-            asm volatile("" ::"v"(bv));
-#pragma unroll
-            for (int r = 0; r < kMR; ++r)
-#pragma unroll
-                for (int k = 0; k < 5; ++k) asm volatile("" : "+v"(w[r][k]));  // (every load in before any store)
-            asm volatile("" ::: "memory");
-            if (lane < e) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ebuf[j * kE + lane], r_out, job.z + lane, 0, 0);
-            if (hb || tb) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bv, r_out, D + bx, 0, 0);
-#pragma unroll
-            for (int r = 0; r < kMR; ++r) {
-                const uint32_t c = lane + 64u * (uint32_t)r;
-                if (c < nch) {
-                    const uint32_t s = src + ((c0 + c) << 4) - D, sh = s & 3u;
-                    const u32x4 v = {__builtin_amdgcn_alignbyte(w[r][1], w[r][0], sh),
-                                     __builtin_amdgcn_alignbyte(w[r][2], w[r][1], sh),
-                                     __builtin_amdgcn_alignbyte(w[r][3], w[r][2], sh),
-                                     __builtin_amdgcn_alignbyte(w[r][4], w[r][3], sh)};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, r_out, (c0 + c) << 4, 0, 0);
-                }
-            }
-        }
-        __syncthreads();
     }
 }
 
