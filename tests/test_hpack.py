@@ -68,6 +68,24 @@ def test_interop_stories_one_batch():
         assert g == w, i
 
 
+def test_interop_stories_any_thread_count(monkeypatch):
+    """The same batch on 1, 3 and 16 host threads: decoders are placed on the apply threads by hash
+    buckets balanced on the scanned work (hpk_hpack.cpp), each decoder's blocks in order on one
+    thread, so every count gives the reference's headers."""
+    pairs, want = [], []
+    stories = list(_stories())
+    for nth in ("1", "3", "16"):
+        monkeypatch.setenv("HPK_HDEC_THREADS", nth)
+        pairs, want = [], []
+        for enc, story in stories:
+            d = hpack.Decoder()
+            for c in story["cases"]:
+                pairs.append((d, bytes.fromhex(c["wire"])))
+                want.append([(n.encode(), v.encode()) for n, v in c["headers"]])
+        got = hpack.decode_blocks(pairs)
+        assert got == want, nth
+
+
 def test_table_size_update_and_eviction():
     d = hpack.Decoder()
     # literal with incremental indexing, new name: 'custom-key: custom-header' (RFC 7541 C.2.1)
