@@ -371,9 +371,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # (rehearsal on a one-GPU box only: HPK_BENCH_DEVICE puts every rank on one device and
+    # HPK_BENCH_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU; never set for a run)
+    if os.environ.get("HPK_BENCH_DEVICE") is not None:
+        local = int(os.environ["HPK_BENCH_DEVICE"])
+    backend = os.environ.get("HPK_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
