@@ -86,14 +86,13 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
         any |= c->long_list[k] != nullptr;
     }
     if (j < 0) {
-        if (any && !c->long_multi) {  // a second stream: events from here on, and one for the past
+        if (any && !c->long_multi) {  // a second stream: events from here on; the past is drained
+            // once, here. (Recording an event on each earlier slot's stream would touch a handle the
+            // caller may have destroyed since — a stream bound with hpk_ctx_set_stream, created and
+            // destroyed by the caller: ADVICE r3. A device-wide wait needs no stream handle.)
             c->long_multi = true;
-            for (int k = 0; k < hpk_ctx::kLongSlots; ++k) {
-                if (!c->long_list[k]) continue;
-                if (!c->long_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[k], hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(c->long_ev[k], c->long_stream[k]));
-                c->long_ev_set[k] = true;
-            }
+            HIP_TRY(hipDeviceSynchronize());
+            for (int k = 0; k < hpk_ctx::kLongSlots; ++k) c->long_ev_set[k] = false;
         }
         j = 0;
         while (j < hpk_ctx::kLongSlots && c->long_list[j]) ++j;
@@ -108,8 +107,8 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
     if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
         if (c->long_ev_set[j])
             HIP_TRY(hipEventSynchronize(c->long_ev[j]));
-        else if (c->long_list[j])
-            HIP_TRY(hipStreamSynchronize(c->long_stream[j]));
+        else if (c->long_list[j])  // single-stream mode on the own stream (foreign streams set events)
+            HIP_TRY(hipStreamSynchronize(c->stream));
         (void)hipFree(c->long_list[j]);
         c->long_list[j] = nullptr;
         c->long_list_cap[j] = 0;
@@ -123,7 +122,10 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
 }
 
 int hpk_long_list_used(hpk_ctx* c, int slot) {
-    if (!c->long_multi) return HPK_E_OK;
+    if (!c->long_multi && c->stream == c->own) return HPK_E_OK;
+    // a stream the context does not own always gets its event: the slot is then never waited on
+    // through the stream handle, which the caller may destroy
+    if (!c->long_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[slot], hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->long_ev[slot], c->stream));
     c->long_ev_set[slot] = true;
     return HPK_E_OK;
@@ -256,6 +258,11 @@ static uint32_t clamp_cap(size_t cap) { return cap > HPK_MAX_OFFSET ? HPK_MAX_OF
 // scratch buffers. With pageable host memory HIP stages the copies itself and the overlap is small:
 // register the arena (hpk_host_register). `trusted`: the offsets were made by the library itself
 // (hpk_hdec_decode_blocks), monotone by construction, so the O(n) host checks are skipped.
+static int queue_chunks(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint8_t* out_blob,
+                        const uint32_t* out_off, uint32_t* out_len, uint8_t* status, uint32_t n, size_t in_bytes,
+                        size_t out_bytes, int chunks, const uint32_t* cut, uint32_t* d_in_off, uint32_t* d_out_off,
+                        uint32_t* d_len);
+
 static int host_begin(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
                       uint32_t n, uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                       uint8_t* status, bool trusted, int* nchunks, uint32_t* cut) {
@@ -296,6 +303,27 @@ static int host_begin(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t i
         cut[j] = lo;
     }
     cut[chunks] = n;
+    // A failure after some chunk's copies were queued leaves DMA into and out of the caller's buffers
+    // (and the pinned staging area the block decoder reuses) in flight: drain the three streams before
+    // returning, so nothing lands after the call has returned.
+    auto drain = [&](int rc) {
+        (void)hipStreamSynchronize(c->h2d);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->d2h);
+        return rc;
+    };
+    if (int e = queue_chunks(fn, c, in_blob, in_off, out_blob, out_off, out_len, status, n, in_bytes, out_bytes,
+                             chunks, cut, d_in_off, d_out_off, d_len))
+        return drain(e);
+    *nchunks = chunks;
+    return HPK_E_OK;
+}
+
+static int queue_chunks(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, const uint32_t* in_off, uint8_t* out_blob,
+                        const uint32_t* out_off, uint32_t* out_len, uint8_t* status, uint32_t n, size_t in_bytes,
+                        size_t out_bytes, int chunks, const uint32_t* cut, uint32_t* d_in_off, uint32_t* d_out_off,
+                        uint32_t* d_len) {
+    int rc;
     HIP_TRY(hipEventRecord(c->ev_run[0], c->stream));  // earlier work on the ctx stream first
     HIP_TRY(hipStreamWaitEvent(c->h2d, c->ev_run[0], 0));
     for (int j = 0; j < chunks; ++j) {
@@ -318,7 +346,6 @@ static int host_begin(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t i
         }
         HIP_TRY(hipEventRecord(c->ev_out[j], c->d2h));
     }
-    *nchunks = chunks;
     return HPK_E_OK;
 }
 

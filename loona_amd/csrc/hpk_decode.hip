@@ -155,6 +155,10 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
             hipLaunchKernelGGL(WAVE_KERNEL(3), grid, block, 0, c->stream, a);
         } else if (g_debug_mode == 2)
             hipLaunchKernelGGL(WAVE_KERNEL(2), grid, block, 0, c->stream, a);
+        else if (g_debug_mode == 6)
+            hipLaunchKernelGGL(WAVE_KERNEL(6), grid, block, 0, c->stream, a);
+        else if (g_debug_mode == 7)
+            hipLaunchKernelGGL(WAVE_KERNEL(7), grid, block, 0, c->stream, a);
         else
             hipLaunchKernelGGL(WAVE_KERNEL(0), grid, block, 0, c->stream, a);
         HIP_TRY(hipGetLastError());

@@ -23,6 +23,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <pthread.h>
 #include <unordered_map>
 #include <thread>
 #include <string>
@@ -193,9 +194,25 @@ class Pool {
     bool stop_ = false;
 };
 
+// One pool per process. After a fork the child inherits the parent's Pool object but none of its
+// threads (run() would wait forever for them), and maybe a mutex some parent thread held: the
+// pthread_atfork child handler forgets it (leaked, never destroyed: its std::thread handles are
+// meaningless in the child) and the child's first call makes a fresh one.
+static Pool* g_pool = nullptr;
+
 Pool& pool() {
-    static Pool p;
-    return p;
+    static const bool registered = [] {
+        pthread_atfork(nullptr, nullptr, [] { __atomic_store_n(&g_pool, (Pool*)nullptr, __ATOMIC_RELEASE); });
+        return true;
+    }();
+    (void)registered;
+    Pool* p = __atomic_load_n(&g_pool, __ATOMIC_ACQUIRE);
+    if (p) return *p;
+    Pool* fresh = new Pool();  // no threads until its first run()
+    Pool* expect = nullptr;
+    if (__atomic_compare_exchange_n(&g_pool, &expect, fresh, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return *fresh;
+    delete fresh;  // another thread installed one first
+    return *expect;
 }
 
 // decode_integer (decoder.rs:67-125): prefix 1..8, at most 5 octets.

@@ -215,6 +215,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         uint32_t cur, ce;
         claim(cur, ce);
         uint32_t gin = 0, gout = 0;
+        uint32_t sens[4] = {0u, 1u, 2u, 3u};  // diagnostic modes 6 / 7 only
         if (cur < ce) {
             gin = a.in_off[cur] + a.in_mis;
             gout = a.out_off[cur] + a.out_mis;
@@ -443,7 +444,25 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 for (;;) {
                     dg_add(9, 1u);
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) lit12_step<kStore, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                    for (int s = 0; s < 2; ++s) {
+                        lit12_step<kStore, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                        // sensitivity diagnostics (libhpk_diag.so): mode 6 adds 16 independent VALU per
+                        // step (4 chains of 4), mode 7 adds 2 conflict-free LDS reads per step, off the
+                        // walk's dependency chain; the kernel's response says which resource binds
+                        if (kMode == 6) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[0]) : "v"(L.X));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[1]) : "v"(L.o));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[2]) : "v"(L.Eb));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[3]) : "v"(L.d1));
+                            }
+                        } else if (kMode == 7) {
+                            const uint32_t r1 = reinterpret_cast<volatile uint32_t*>(smem)[lane];
+                            const uint32_t r2 = reinterpret_cast<volatile uint32_t*>(smem)[64u + lane];
+                            sens[0] += r1 ^ r2;
+                        }
+                    }
                     const bool fin = !L.prog;  // no progress in the last step: ended (a fixed point) or idle
                     if (__any(fin)) {
                         const bool sw = fin & nv;
@@ -461,6 +480,8 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 Lend = L.o;
             }
             stamp(6);
+            if ((kMode == 6 || kMode == 7) && (kMode == 7 ? sens[0] : sens[0] ^ sens[1] ^ sens[2] ^ sens[3]) == 0x5EB51u)
+                a.status[0] = 9u;  // (never: keeps the diagnostic work alive)
             // results: the first slot's from its saved end state, the second's from the walk
             {
                 const uint32_t Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (e1.x >> 16) * 8u;

@@ -8,7 +8,9 @@ bytes, with u32 offsets rebased per shard. Two ways to use it:
 * root-resident batch (`scatter_decode_gather`): rank 0 holds the whole batch (e.g. literals
   gathered from many connections on one host thread), sends each rank its shard, every rank
   decodes locally, results come back to rank 0. Unequal shard sizes go point-to-point
-  (send/recv), which both RCCL ("nccl") and gloo support; sizes travel first.
+  (send/recv); sizes travel first. The backend must carry the tensors' device: RCCL ("nccl") for
+  GPU tensors, gloo for CPU tensors (gloo has no point-to-point for device tensors: posted anyway,
+  the sends never complete). A mismatch is refused before the first collective.
 """
 
 from __future__ import annotations
@@ -90,30 +92,43 @@ def compact_offsets(out_len, m):
 
 def compact(out_blob, out_off, out_len, m, total, chunk=1 << 28):
     """The decoded bytes of m literals (literal i at out_off[i], out_len[i] bytes: the region layout a
-    decode writes) laid end to end: a uint8 tensor of `total` bytes on the same device (no host sync:
-    total is known). Built in pieces of ~`chunk` bytes so the index tensor stays bounded."""
+    decode writes) laid end to end: a uint8 tensor of `total` bytes on the same device. Built in
+    pieces of ~`chunk` bytes so the index tensor stays bounded; the pieces' literal and byte bounds
+    come to the host in ONE read (total is known, so nothing else waits on the device)."""
     import torch
 
     dev = out_blob.device
     res = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
-    if total == 0:
+    if total == 0 or m == 0:
         return res[:0]
     ln = out_len[:m].to(torch.int64)
     src = out_off[:m].to(torch.int64) & 0xFFFFFFFF
     coff = compact_offsets(out_len, m)
-    # literal ranges of about `chunk` output bytes each (a host read of the cut points: one per piece)
-    cuts = torch.searchsorted(coff, torch.arange(0, total + chunk, chunk, device=dev, dtype=torch.int64)).tolist()
-    cuts = sorted(set([0] + [min(c, m) for c in cuts] + [m]))
-    for a, b in zip(cuts[:-1], cuts[1:]):
-        if a == b:
-            continue
-        x0, x1 = int(coff[a].item()), int(coff[b].item())
-        if x1 == x0:
+    # literal ranges of about `chunk` output bytes each: cut indices and their byte offsets together
+    cuts = torch.searchsorted(coff, torch.arange(0, total + chunk, chunk, device=dev, dtype=torch.int64))
+    cuts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cuts.clamp_(max=m),
+                      torch.full((1,), m, dtype=torch.int64, device=dev)])
+    host = torch.stack([cuts, coff[cuts]]).tolist()  # the one host read
+    bounds = sorted(set(zip(host[0], host[1])))
+    for (a, x0), (b, x1) in zip(bounds[:-1], bounds[1:]):
+        if a == b or x1 == x0:
             continue
         idx = torch.repeat_interleave(src[a:b] - (coff[a:b] - x0), ln[a:b], output_size=x1 - x0)
         idx += torch.arange(x1 - x0, device=dev, dtype=torch.int64)
         res[x0:x1] = out_blob[idx]
     return res
+
+
+def check_backend(dist, group, dev):
+    """Refuse a backend that cannot carry tensors on `dev` (every rank makes the same test, so all of
+    them raise, before any message is posted): gloo has no device-tensor point-to-point (posted
+    anyway, the sends never complete: gpurun_out/rehearse2/n2_e2e.json of round 3), RCCL no host
+    tensors."""
+    be = str(dist.get_backend(group)).lower()
+    if dev.type == "cuda" and be == "gloo":
+        raise ValueError("scatter_decode_gather: the gloo backend cannot send device tensors; use nccl (RCCL)")
+    if dev.type == "cpu" and be == "nccl":
+        raise ValueError("scatter_decode_gather: the nccl (RCCL) backend cannot send host tensors; use gloo")
 
 
 def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
@@ -129,8 +144,9 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
     shard with one grouped send/recv round. Every owner then lays its shards' decoded bytes end to
     end (only out_len bytes per literal travel back, not the regions' slack), one all-reduce tells
     root every shard's decoded size, and the bytes, out_len and status come back in one more grouped
-    round. Host synchronisation: the size broadcast and the all-reduce, once each, whatever the
-    number of shards. With gloo and CPU tensors the same code runs on the host (tests/test_shard.py).
+    round. Host synchronisation: the size broadcast, the all-reduce and one read of the piece bounds
+    per owned shard in `compact`. Refusals (a backend that cannot carry the device, a bad shard on
+    root, a failed decode on any rank) make EVERY rank raise, never a hang. With gloo and CPU tensors the same code runs on the host (tests/test_shard.py).
     Returns on root the list of (decoded bytes laid end to end, their int64 offsets [m+1], out_len,
     status) in shard order; None elsewhere."""
     import torch
@@ -138,14 +154,24 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = torch.device(device) if device is not None else torch.device("cpu")
-    # 1. shard sizes, from root to every rank: [S] then S x (literals, blob bytes)
-    cnt = torch.tensor([len(shards) if rank == root else 0], dtype=torch.int64, device=dev)
+    check_backend(dist, group, dev)
+    # 1. shard sizes, from root to every rank: [S] then S x (literals, blob bytes). Root checks the
+    # shards BEFORE the count goes out and sends S = -1 on a bad one, so every rank raises (a root
+    # that raised after the broadcast would leave the others waiting in the next one)
+    err = None
+    if rank == root:
+        try:
+            for s, (b, off) in enumerate(shards):
+                _check(off, f"shard {s} offsets", ("int32", "uint32"))
+                _check(b, f"shard {s} blob", ("uint8",))
+        except ValueError as e:
+            err = e
+    cnt = torch.tensor([(len(shards) if err is None else -1) if rank == root else 0], dtype=torch.int64, device=dev)
     dist.broadcast(cnt, root, group=group)
     S = int(cnt.item())
+    if S < 0:
+        raise err if err is not None else ValueError("scatter_decode_gather: root refused its shards")
     if rank == root:
-        for s, (b, off) in enumerate(shards):
-            _check(off, f"shard {s} offsets", ("int32", "uint32"))
-            _check(b, f"shard {s} blob", ("uint8",))
         meta = torch.tensor([[int(o.numel()) - 1, int(b.numel())] for b, o in shards], dtype=torch.int64,
                             device=dev).reshape(S, 2)
     else:
@@ -175,19 +201,31 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None):
             local[s] = shards[s]
     _p2p(dist, ops, group)
     # 3. decode the local shards; every shard's decoded size, on the device
-    res = {s: decode_fn(*local[s]) for s in mine}
-    tot = torch.zeros(max(S, 1), dtype=torch.int64, device=dev)
-    for s in mine:
-        ob, oo, ol, st = res[s]
-        _check(ol, f"shard {s} out_len", ("int32", "uint32"))
-        _check(st, f"shard {s} status", ("uint8",))
-        m = sizes[s][0]
-        if m:
-            tot[s] = ol[:m].to(torch.int64).sum()
+    # (an owner whose decode_fn fails or returns tensors the wire would misread does not raise here:
+    # it flags the error in the all-reduce below, so every rank raises together instead of the
+    # others waiting for it in the collective)
+    res, err = {}, None
+    tot = torch.zeros(S + 1, dtype=torch.int64, device=dev)  # [S] = ranks that failed
+    try:
+        for s in mine:
+            res[s] = decode_fn(*local[s])
+            ob, oo, ol, st = res[s]
+            _check(ol, f"shard {s} out_len", ("int32", "uint32"))
+            _check(st, f"shard {s} status", ("uint8",))
+            m = sizes[s][0]
+            if m:
+                tot[s] = ol[:m].to(torch.int64).sum()
+    except Exception as e:  # noqa: BLE001 -- re-raised after the collective
+        err = e
+        tot.zero_()
+        tot[S] = 1
     # 4. one all-reduce: every rank (root included) learns every shard's decoded size
-    if S:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
     totals = tot.tolist()
+    if totals[S]:
+        if err is not None:
+            raise err
+        raise RuntimeError(f"scatter_decode_gather: {totals[S]} rank(s) failed to decode their shards")
     # 5. the owners lay their shards' bytes end to end; bytes, out_len and status go to root
     packed = {s: compact(*res[s][:3], sizes[s][0], int(totals[s])) for s in mine}
     out, ops = {}, []

@@ -805,3 +805,100 @@ def test_h2_frames_in_pinned_arena_on_device(codec):
     from test_h2 import replay_in_arena
 
     replay_in_arena(codec, pin=True)
+
+
+def _large_literals():
+    """Literals of 16 KiB - 1 MiB encoded: the reference accepts string lengths up to
+    ~2^28 (crates/loona-hpack/src/decoder.rs:96-99) and concatenates CONTINUATION payloads into one
+    block (crates/loona/src/h2/server.rs:1625-1633), so one literal can be a whole large header."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(4096)
+    text = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;,/.:ABCDEFGHIJ ", np.uint8)
+
+    def text_enc(nbytes):  # a valid literal of exactly nbytes encoded bytes (text prefix, EOS padding)
+        s = huffman_encode(rng.choice(text, nbytes * 2).tobytes())[:nbytes]
+        return bytes(s)
+
+    lits = []
+    for nb in (16384, 65535, 65536, 65537, 262144, 1 << 20):
+        lits.append(text_enc(nb))  # cut mid-code: padding error or a valid end, as the oracle says
+        lits.append(huffman_encode(rng.choice(text, nb + nb // 3).tobytes()))  # valid text
+        lits.append(rng.integers(0, 40, 17, dtype=np.uint8).tobytes())  # a short one between
+    lits.append(huffman_encode(rng.integers(0, 256, 120000, dtype=np.uint8).tobytes()))  # ~270 KB, long codes
+    eos = (1 << 30) - 1
+    for m in (70000, 140001):  # EOS 40 bits before the end of a ~64/128 KB literal
+        body = huffman_encode(b"x" * m)
+        bits = int.from_bytes(body, "big") >> (len(body) * 8 - m * 7)  # 'x' is 7 bits
+        v = (((bits << 30) | eos) << 10) | 0x3FF
+        tot = m * 7 + 40
+        pad = (-tot) % 8
+        lits.append(((v << pad) | ((1 << pad) - 1)).to_bytes((tot + pad) // 8, "big"))
+    body = bytearray(huffman_encode(b"content-security-policy: default-src 'self'" * 3000))
+    body[-1] &= 0xF0  # bad padding after ~100 KB of valid codes
+    lits.append(bytes(body))
+    lits.append(huffman_encode(b"z" * 80000) + b"\xff")  # too much padding
+    lits.append(b"\xff" * 70000)  # EOS at once
+    return lits
+
+
+def test_large_literals(codec):
+    """16 KiB, 64 KiB +- 1, 256 KiB and 1 MiB encoded literals through both kernels (they exceed any
+    fill window: the long-literal phase or the one-lane global path) against the oracle: valid, cut
+    mid-code, long codes, EOS near the end, bad and too-long padding; then at exact-bound regions on
+    an unaligned base (+3) with guard bytes around the output."""
+    lits = _large_literals()
+    blob, off = pack(lits)
+    ref = oracle_decode_batch(blob, off)
+    compare_batches(gpu_decode(codec, blob, off), ref, "large literals")
+    compare_batches(gpu_decode(codec, blob, off, shift=5), ref, "large literals, input at +5")
+    bound = [int(off[i + 1] - off[i]) * 8 // 5 for i in range(len(off) - 1)]
+    got, guard = _decode_regions(codec, blob, off, bound, shift=3)
+    compare_batches(got, ref, "large literals, exact-bound regions at +3")
+    assert (guard == 0xAB).all()
+
+
+def test_stream_destroyed_then_another_stream(codec):
+    """a context bound to a caller-created stream A (hpk_ctx_set_stream) that the caller
+    then destroys must not touch A's handle when a second stream B first uses it (the switch to
+    per-slot events). Every result checked against the oracle."""
+    import ctypes
+
+    from loona_amd import synth
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    w = synth.config2(n=3000, seed=17)
+    want = oracle_decode_batch(w.enc_blob, w.enc_off)
+    streams = []
+    try:
+        for k in range(3):
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            codec.set_stream(s.value)
+            torch.cuda.synchronize()
+            compare_batches(gpu_decode(codec, w.enc_blob, w.enc_off), want, f"stream {k}")
+            assert hip.hipStreamSynchronize(s) == 0
+            assert hip.hipStreamDestroy(s) == 0
+            streams.append(s.value)
+    finally:
+        codec.set_stream(torch.cuda.current_stream())
+    compare_batches(gpu_decode(codec, w.enc_blob, w.enc_off), want, "back on torch's stream")
+
+
+def test_hpack_blocks_many_chunks_on_device(codec):
+    """the block decoder's overlap of its apply threads with the device chunks (threads
+    waiting on chunk j's copy-out while later chunks still copy) with enough bytes for the host
+    pipeline to cut the batch into its 8 chunks: every interop story six times over under fresh
+    decoders, every block compared with the fixture's header list."""
+    from loona_amd import hpack
+
+    inter = load("interop.json.gz")
+    pairs, want = [], []
+    for _ in range(6):
+        for enc in sorted(inter):
+            for story in inter[enc]:
+                d = hpack.Decoder()
+                for c in story["cases"]:
+                    pairs.append((d, bytes.fromhex(c["wire"])))
+                    want.append([(n.encode(), v.encode()) for n, v in c["headers"]])
+    assert hpack.decode_blocks(pairs, codec) == want

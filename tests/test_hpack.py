@@ -235,3 +235,47 @@ def test_dynamic_table_churn_matches_restatement():
     assert sum(not isinstance(x, hpack.DecoderError) for x in want) > 300
     for i, (g, w) in enumerate(zip(got, want)):
         assert g == w, (i, pairs[i][1][:64].hex())
+
+
+def test_block_decoder_after_fork(monkeypatch):
+    """the block decoder's process-wide worker pool survives a fork. The parent decodes
+    on 16 threads (the pool's threads start), forks, and the child decodes the same batch again: it
+    must get a fresh pool (the parent's threads do not exist in the child) instead of waiting forever
+    for them. The child runs under a time limit; its exit code says whether its headers matched."""
+    import os
+    import signal
+    import time
+
+    monkeypatch.setenv("HPK_HDEC_THREADS", "16")
+
+    def batch():
+        pairs, want = [], []
+        for enc, story in _stories():
+            d = hpack.Decoder()
+            for c in story["cases"]:
+                pairs.append((d, bytes.fromhex(c["wire"])))
+                want.append([(n.encode(), v.encode()) for n, v in c["headers"]])
+        return pairs, want
+
+    pairs, want = batch()
+    assert hpack.decode_blocks(pairs) == want
+    pairs, want = batch()
+    pid = os.fork()
+    if pid == 0:  # child: no pytest machinery, just the decode and an exit code
+        code = 1
+        try:
+            code = 0 if hpack.decode_blocks(pairs) == want else 2
+        finally:
+            os._exit(code)
+    deadline = time.time() + 120
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() > deadline:
+            os.kill(pid, signal.SIGKILL)
+            os.waitpid(pid, 0)
+            pytest.fail("the child's block decode hung after fork")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+    assert hpack.decode_blocks(pairs) == want  # the parent's pool still works
