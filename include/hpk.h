@@ -125,13 +125,15 @@ int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
                      uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                      uint8_t* status, int flags);
 
-/* Which decode kernel a context's batches use. Both give identical results (the parity tests run
+/* Which decode kernel a context's batches use. All give identical results (the parity tests run
  * every case through each); they differ in speed by batch size. HPK_DECODE_AUTO (the default): the
- * wave-fill kernel (decode v25) for batches of at least 4M literals, the workgroup-fill kernel
- * (v24) below that. */
+ * lane-per-literal kernel with no LDS staging for batches of at most 16Ki literals (one loona
+ * thread's read_headers call: latency-bound), the workgroup-fill kernel below 4M literals, the
+ * wave-fill kernel from 4M on. */
 #define HPK_DECODE_AUTO 0
 #define HPK_DECODE_FILL 1 /* workgroup fills: one fill at a time per CU, barriers between fills */
 #define HPK_DECODE_WAVE 2 /* wave fills: every wave its own fills, no barriers between them */
+#define HPK_DECODE_TINY 3 /* one lane per literal straight from global memory (small batches) */
 int hpk_ctx_set_decode_kernel(hpk_ctx* ctx, int kind);
 
 /* Read and clear the context's sticky device error flag (after HPK_ASYNC calls; synchronises the

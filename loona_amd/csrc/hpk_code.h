@@ -74,11 +74,24 @@ static const uint8_t HPK_CODE_LEN[HPK_NSYM] = {
 #define HPK_L2_CODES(e) (((e) >> 28) & 3u)
 #define HPK_L2_TWO(e) (((e) >> 29) & 1u)
 
+// LUT3 (decode v28, the wave kernel): the same codes in a layout whose "bits held" is a whole byte, so
+// the body step (lit12_body) shifts by it and adds it with sub-dword (SDWA) operand selection, no
+// bfe:
+//   [7:0] sym0  [15:8] bits held  [23:16] sym1  [25:24] codes held  [29:26] len0 (15: none)
+//   [31] fewer than two codes
+// The checked step reads len0 from [29:26] and the two codes' length as "bits held" when [31] is
+// clear (lutc<kLut3>).
+#define HPK_L3_HELD(e) (((e) >> 8) & 0xFFu)
+#define HPK_L3_CODES(e) (((e) >> 24) & 3u)
+#define HPK_L3_LEN0(e) (((e) >> 26) & 15u)
+#define HPK_L3_NOTTWO 0x80000000u
+
 struct hpk_tables {
     uint32_t code[HPK_NSYM];   // right-aligned canonical code
     uint8_t len[HPK_NSYM];     // code length in bits
     uint32_t lut[HPK_LUT_SIZE];
     uint32_t lut2[HPK_LUT_SIZE];
+    uint32_t lut3[HPK_LUT_SIZE];
     uint16_t lo[HPK_LO_SIZE];
     uint8_t t8[256];  // symbol of the <=8-bit code that prefixes each 8-bit window (0 past LIM8)
 };
@@ -163,6 +176,11 @@ static inline int hpk_build_tables(hpk_tables* t) {
         }
         t->lut[v] = e;
         t->lut2[v] = e2;
+    }
+    for (uint32_t v = 0; v < HPK_LUT_SIZE; ++v) {  // LUT3 from LUT2
+        const uint32_t e2 = t->lut2[v], codes = HPK_L2_CODES(e2);
+        t->lut3[v] = (e2 & 0xFFu) | (HPK_L2_HELD(e2) << 8) | (e2 & 0x00FF0000u) | (codes << 24) |
+                     ((codes ? HPK_L2_LEN0(e2) : 15u) << 26) | (codes < 2 ? HPK_L3_NOTTWO : 0u);
     }
     return 0;
 }

@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.26 gfx950 decode v26 (batches >= 4M literals: wave fills, each wave with its own LDS window and image, one chunk at a time handed out by guided self-scheduling, lane walk addressed from the LDS base, longest-first queue by an LDS counting sort, no workgroup barriers between fills; smaller batches: v24 workgroup fills; both: alignbit lane step with two LUT2 lookups, unconditional byte stores, static snake; long literals one lane each streaming from HBM after the fills, per workgroup); encode v4 (byte-balanced workgroup ranges, segmented scan, branch-free run accumulator with prefix-OR dword stores, phantom runs, LDS image, live chunks only)"
+#define HPK_VERSION "hpk 0.28 gfx950 decode v28 (batches >= 4M literals: wave fills, each wave with its own LDS window and image, chunks by guided self-scheduling, longest-first queue; 16Ki..4M: workgroup fills; <= 16Ki: one lane per literal straight from global memory; fills and long-literal phase: body steps with no fit tests (byte-wide bits-held LUT3 in the wave kernel) while >= 29 bits are left, then checked tails, two literals per lane at once; long literals one lane each streaming from HBM after the fills); encode v4 (byte-balanced workgroup ranges, segmented scan, run accumulator, LDS image, live chunks only)"
 
 static thread_local std::string t_last_error;
 
@@ -56,6 +56,9 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     if ((e = hipMalloc(&c->d_lut2, sizeof(t->lut2))) != hipSuccess) return fail("hipMalloc lut2", e);
     if ((e = hipMemcpy(c->d_lut2, t->lut2, sizeof(t->lut2), hipMemcpyHostToDevice)) != hipSuccess)
         return fail("upload lut2", e);
+    if ((e = hipMalloc(&c->d_lut3, sizeof(t->lut3))) != hipSuccess) return fail("hipMalloc lut3", e);
+    if ((e = hipMemcpy(c->d_lut3, t->lut3, sizeof(t->lut3), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail("upload lut3", e);
     if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
     if ((e = hipMalloc(&c->d_t8, sizeof(t->t8))) != hipSuccess) return fail("hipMalloc t8", e);
     if ((e = hipMemcpy(c->d_t8, t->t8, sizeof(t->t8), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload t8", e);
@@ -137,6 +140,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->d_lut);
     (void)hipFree(c->d_lut2);
+    (void)hipFree(c->d_lut3);
     (void)hipFree(c->d_lo);
     (void)hipFree(c->d_t8);
     (void)hipFree(c->d_codes);
@@ -203,7 +207,7 @@ int hpk_ctx_pinned(hpk_ctx* c, size_t bytes, void** p) {
 }
 
 extern "C" int hpk_ctx_set_decode_kernel(hpk_ctx* c, int kind) {
-    if (!c || kind < HPK_DECODE_AUTO || kind > HPK_DECODE_WAVE) return hpk_set_err_msg("bad decode kernel", HPK_E_INVAL);
+    if (!c || kind < HPK_DECODE_AUTO || kind > HPK_DECODE_TINY) return hpk_set_err_msg("bad decode kernel", HPK_E_INVAL);
     c->decode_kernel = kind;
     return HPK_E_OK;
 }

@@ -24,6 +24,7 @@
 // code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
 #include <stdlib.h>
 
+#include "hpk_tiny.h"
 #include "hpk_wave.h"
 
 using namespace hpkdec;
@@ -80,6 +81,10 @@ extern "C" int hpk_debug_stamps(unsigned long long* host, size_t cap_entries) {
 }
 #endif
 
+#ifndef HPK_TINY_MAX
+#define HPK_TINY_MAX 16384u  // batches of at most this many literals: hpk_decode_tiny (AUTO)
+#endif
+
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     DecodeArgs a;
     const uintptr_t ip = (uintptr_t)b.in_blob;
@@ -97,10 +102,19 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.lo = c->d_lo;
     a.lut = c->d_lut;
     a.lut2 = c->d_lut2;
+    a.lut3 = c->d_lut3;
     a.dbg = nullptr;
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
+    const bool tiny = c->decode_kernel == HPK_DECODE_TINY || (c->decode_kernel == HPK_DECODE_AUTO && b.n <= HPK_TINY_MAX);
+    if (tiny) {  // no long-literal list, no LDS: one lane per literal (hpk_tiny.h)
+        a.long_list = nullptr;
+        a.long_min = a.long_big = 0;
+        hipLaunchKernelGGL(hpk_decode_tiny, dim3((b.n + 63u) / 64u), dim3(64), 0, c->stream, a);
+        HIP_TRY(hipGetLastError());
+        return HPK_E_OK;
+    }
     uint32_t* ll = nullptr;
     int lslot = 0;
     if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
@@ -135,7 +149,7 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
             case 5: hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, 224u, true, 2>), grid, block, 0, c->stream, a); break;
             // (the least chunk of the guided hand-out, 128-1024 literals: within the noise, r3l; the 3072 /
             // 5888 split won over 3328-3840 B windows, whose fourth prefetch round spills, r3i; dword
-            // output by LDS masked OR, bench/legacy_wave_mk.h: 1223-1229 us, r3o)
+            // output by LDS masked OR, code in git history: 1223-1229 us, r3o)
             default: hipLaunchKernelGGL((WAVE_KERNEL(0)), grid, block, 0, c->stream, a); break;
         }
         HIP_TRY(hipGetLastError());

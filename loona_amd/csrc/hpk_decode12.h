@@ -21,8 +21,8 @@
 //   * Stores (v14): a step's (up to) four byte stores are unconditional, a byte that is not output
 //     going to the lane's dummy slot (no exec-mask branch around each ds_write_b8).
 // The variants measured along the way and not taken (whole-wave long literals, the segment stream,
-// dynamic slots, dword stores, deferred write-back, ...) live in bench/legacy_decode12.h for the
-// harness; DESIGN.md §4.1 has their numbers.
+// dynamic slots, dword stores, deferred write-back, ...) were timed in the round 1-3 harness
+// (bench/legacy_decode12.h, removed in round 4; git history keeps it); DESIGN.md has their numbers.
 #pragma once
 #include "hpk_decode_kernel.h"
 
@@ -35,6 +35,9 @@
 #define HPK_STAGGER 1
 #define HPK_STAGGER_PH 2
 #define HPK_LATE_FIN 1
+#ifndef HPK_FILL_BODY
+#define HPK_FILL_BODY 1  // v28: body steps + two-at-once checked tails in the fill kernel too
+#endif
 
 namespace hpkdec {
 
@@ -68,13 +71,24 @@ __device__ __forceinline__ uint32_t win_at(const uint32_t* __restrict__ win32, u
 
 // The codes one table entry decodes with rem bits left: ok1 / ok2 = its first / second code fits
 // inside the literal; returns the bits they use.
+template <int kTab = 2>  // the table layout: 2 = LUT2, 3 = LUT3 (hpk_code.h)
 __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
-    // a length field the entry does not hold is 63, past any clamped rem (and t1 >= l1: ok2 => ok1)
+    // a length field the entry does not hold is 15, past any clamped rem (and t1 >= l1: ok2 => ok1)
     const uint32_t rc = min(rem, HPK_LUT2_CLAMP);
+    if (kTab == 3) {
+        const uint32_t l1 = HPK_L3_LEN0(e), t1 = HPK_L3_HELD(e);
+        ok1 = l1 <= rc;
+        ok2 = (t1 <= rc) & (e < HPK_L3_NOTTWO);
+        return ok2 ? t1 : (ok1 ? l1 : 0u);
+    }
     const uint32_t l1 = HPK_L2_LEN0(e), t1 = HPK_L2_LEN01(e);
     ok1 = l1 <= rc;
     ok2 = t1 <= rc;
     return ok2 ? t1 : (ok1 ? l1 : 0u);
+}
+template <int kTab>
+__device__ __forceinline__ bool lut_nottwo(uint32_t e) {
+    return kTab == 3 ? e >= HPK_L3_NOTTWO : e >= HPK_LUT2_NOTTWO;
 }
 
 // The decoded bytes of an entry, packed little-endian and zero above the g = ok1 + ok2 of them.
@@ -103,6 +117,8 @@ struct Lit12 {
     uint32_t st;          // hpk_status set by the walk (EOS, or padding found by the long-code branch)
     uint32_t idx;         // literal index in the fill
     bool prog;            // the last step consumed a code or took the long-code branch
+    bool more;            // (kMore steps) the walk may go on: the last step used both entries whole, or
+                          // decoded a long code; false once a step has proved that no code fits
     bool act;             // holds a fast-path literal not yet finalised
 };
 
@@ -119,9 +135,10 @@ __device__ __forceinline__ void lit12_load(Lit12& L, const uint32_t* __restrict_
 // going to the lane's dummy slot out8[dmy] (no exec-mask branch around each store); kChecked
 // (diagnostic mode 4) checks every store against the literal's capacity, kNoStore (mode 2) stores
 // nothing.
-template <int kStore, bool kP1 = false>  // kP1: a lookup's second byte stored at (address) + 1 by the
-                                         // store's offset (the wave kernel; in the fill kernel's
-                                         // register budget the extra live dmy - 1 spills)
+template <int kStore, bool kP1 = false,   // kP1: a lookup's second byte stored at (address) + 1 by the
+          int kTab = 2,                  // store's offset (the wave kernel; in the fill kernel's
+          bool kMore = false>            // register budget the extra live dmy - 1 spills); kTab: lut12;
+                                         // kMore: set L.more (the tails of decode v27)
 __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                            const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8,
                                            uint32_t dmy = 0) {
@@ -130,11 +147,12 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     const uint32_t rem = L.Eb - L.X;
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
     bool a1, a2;
-    const uint32_t u1 = lut12(e1, rem, a1, a2);
+    const uint32_t u1 = lut12<kTab>(e1, rem, a1, a2);
     uint32_t use = u1;
     // a code longer than 12 bits (or EOS) starts here and may still fit (with more than 12 bits
     // left, any code the entry holds fits: no first code <=> the entry has none)
     bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
+    bool more2 = false;
     if (kStore == kPred) {
         out8[a1 ? L.o : dmy] = (uint8_t)e1;
         if (kP1)
@@ -148,15 +166,18 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     L.o += (uint32_t)a1 + (uint32_t)a2;
     {
         // the first entry was consumed whole: look the next bits up too
-        const bool cont = a1 & (a2 | (e1 >= HPK_LUT2_NOTTWO));
+        const bool cont = a1 & (a2 | lut_nottwo<kTab>(e1));
         const uint32_t w2 = w << u1;
         const uint32_t rem2 = rem - u1;
         const uint32_t e2 = lut[w2 >> (32 - HPK_LUT_BITS)];
         bool b1, b2;
-        const uint32_t u2 = lut12(e2, rem2, b1, b2);
+        const uint32_t u2 = lut12<kTab>(e2, rem2, b1, b2);
         park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
         b1 &= cont;
         b2 &= cont;
+        // both entries used whole: more codes may follow (otherwise one of them held a code that does
+        // not fit, or none with <= 12 bits left: the walk has ended here, huffman.rs:100-123)
+        more2 = b1 & (b2 | lut_nottwo<kTab>(e2));
         if (kStore == kPred) {
             out8[b1 ? L.o : dmy] = (uint8_t)e2;
             if (kP1)
@@ -177,6 +198,7 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     L.d2 = cross ? d3 : L.d2;
     L.X = xn;
     L.prog = a1 | park;
+    if (kMore) L.more = park | more2;
     if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
         const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
         uint32_t s, len;
@@ -186,9 +208,11 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
         if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
             L.st = HPK_PADDING_TOO_LARGE;
             L.Eb = L.X;
+            if (kMore) L.more = false;
         } else if (eos) {  // huffman.rs:112-116
             L.st = HPK_EOS_IN_STRING;
             L.Eb = L.X;
+            if (kMore) L.more = false;
         } else {
             put8(out8, L.o, s, L.oend, kStore);
             L.o += 1;
@@ -196,6 +220,69 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
             lit12_load(L, win32);
         }
     }
+}
+
+// Body step (decode v27): the same two lookups with NO fit tests, for a literal with at least
+// kBodyMin bits left before the step. A step consumes <= 24 bits, so every code the two entries hold
+// ends inside the literal, and >= 13 bits are left after it. The stores are unconditional at the
+// lane's own output positions: an entry's second byte when it holds one code (or both bytes when it
+// holds none) is garbage that the next store overwrites, or lies past the decoded bytes inside the
+// literal's own region (see kBodyMin). Lengths come from the entries' "bits held" and "codes held" fields: ~25 VALU per
+// step against lit12_step's ~48. A lookup that holds no code (a 13..30-bit code or EOS) takes the
+// checked leading-ones branch of lit12_step; `body` says whether the next step may be a body step.
+#ifndef HPK_BODY_MIN
+#define HPK_BODY_MIN 29
+#endif
+// 24 bits a step may consume + 5: after a body step >= 5 bits are left, so when the decoded bytes end
+// there the decoded length is below the bound (a code is >= 5 bits) and a garbage byte at the next
+// output position stays in the region; a lookup holding no code has >= 29 - 12 > 12 bits left, so it
+// always takes the leading-ones branch (whose symbol overwrites the garbage)
+constexpr uint32_t kBodyMin = HPK_BODY_MIN;
+
+template <int kStore, int kTab = 2>
+__device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, bool& body) {
+    const uint32_t d3 = win32[(L.X >> 5) + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+    const uint32_t u1 = kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
+    const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
+    const uint32_t u2 = kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
+    const uint32_t o1 = L.o + (kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1));
+    if (kStore != kNoStore) {
+        out8[L.o] = (uint8_t)e1;
+        (out8 + 1)[L.o] = (uint8_t)(e1 >> 16);
+        out8[o1] = (uint8_t)e2;
+        (out8 + 1)[o1] = (uint8_t)(e2 >> 16);
+    }
+    L.o = o1 + (kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2));
+    const uint32_t xn = L.X + u1 + u2;
+    const bool cross = (xn ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xn;
+    if (u2 == 0u) {  // e2 holds no code (nor e1, if u1 == 0): a 13..30-bit code or EOS at X; > 12 bits are
+                     // left (>= kBodyMin - 12 before this lookup), so the leading-ones branch of lit12_step applies
+        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+        uint32_t sy, len;
+        bool eos;
+        lo_decode(wp, lo, sy, len, eos);
+        const uint32_t r = L.Eb - L.X;
+        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+            L.st = HPK_PADDING_TOO_LARGE;
+            L.Eb = L.X;
+        } else if (eos) {  // huffman.rs:112-116
+            L.st = HPK_EOS_IN_STRING;
+            L.Eb = L.X;
+        } else {
+            if (kStore != kNoStore) out8[L.o] = (uint8_t)sy;
+            L.o += 1;
+            L.X += len;
+            lit12_load(L, win32);
+        }
+    }
+    body = L.Eb - L.X >= kBodyMin;
 }
 
 // Final status of a literal whose walk has stopped; a status set by the walk wins.
@@ -680,7 +767,54 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             const uint32_t t2 = 2u * G::kBlock - 1u - t1;
             bool nv = t2 < kq;  // a second literal is waiting in N
             load(N, t2);
-            if (kLate) {
+            if (kLate && HPK_FILL_BODY) {
+                // v28 (as the wave kernel, hpk_wave.h): body steps (lit12_body) while a literal has >=
+                // kBodyMin bits left, slot t1's body then slot t2's; then both tails at once with
+                // checked steps that clear `more` once the walk has ended
+                bool body = L.Eb - L.X >= kBodyMin;
+                uint32_t aX = L.X, aO = L.o, aSt = L.st;
+                bool aAct = L.act, onA = true;
+                for (;;) {
+#pragma unroll
+                    for (int s = 0; s < kRefillN; ++s)
+                        if (body) lit12_body<kStore>(L, win32, s_lut, s_lo, s_out, body);
+                    if (kMode == 3) n_steps += kRefillN;
+                    if (kPfLoop && pf_i < (uint32_t)kPfN) pf_part(pf_i++);
+                    if (__any(!body)) {
+                        const bool sw = !body & onA;
+                        if (sw) {
+                            aX = L.X;
+                            aO = L.o;
+                            aSt = L.st;
+                            aAct = L.act;
+                            L = N;
+                            onA = false;
+                            body = L.Eb - L.X >= kBodyMin;
+                        }
+                        if (!__any(body)) break;
+                    }
+                }
+                N = L;
+                {
+                    const uint2 e = lq[min(t1, kq - 1)];
+                    L.X = aX;
+                    L.o = aO;
+                    L.st = aSt;
+                    L.act = aAct;
+                    L.Eb = aSt != HPK_OK ? aX : (e.x & 0xFFFFu) * 8u + 31u + (aAct ? (e.x >> 16) * 8u : 0u);
+                    L.o0 = (e.y >> 12) & 0x1FFFFu;
+                    L.idx = e.y & 0xFFFu;
+                    lit12_load(L, win32);
+                }
+                L.more = L.Eb - L.X >= 5u;
+                N.more = N.Eb - N.X >= 5u;
+                while (__any(L.more | N.more)) {
+                    if (L.more) lit12_step<kStore, false, 2, true>(L, win32, s_lut, s_lo, s_out, dmy);
+                    if (N.more) lit12_step<kStore, false, 2, true>(N, win32, s_lut, s_lo, s_out, dmy);
+                }
+                if (L.act) s_lenst[L.idx] = (L.o - L.o0) | (lit12_status(L) << 24);
+                if (N.act) s_lenst[N.idx] = (N.o - N.o0) | (lit12_status(N) << 24);
+            } else if (kLate) {
                 // v22: a lane's first literal that ends leaves only its end state (bit and output
                 // positions, walk status) in three registers as the second one starts; lengths and
                 // statuses (the padding check) are made once per lane after the loop, not in every

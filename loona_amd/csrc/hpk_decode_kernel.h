@@ -1,7 +1,7 @@
 // hpk_decode_kernel.h — building blocks of the gfx950 decode kernel (hpk_decode12.h; design
 // notes in hpk_decode.hip): kernel arguments, LDS carve-up, the code-by-code byte path, the
-// longest-first bucket, fill prefetch. Earlier kernels built on them (v3-v11) live in
-// bench/legacy_decode*.h for comparison runs and are not part of libhpk.so.
+// longest-first bucket, fill prefetch. Earlier kernels built on them (v3-v11) are in git history
+// (bench/legacy_decode*.h until round 3).
 #pragma once
 #include <stdint.h>
 
@@ -29,6 +29,7 @@ struct DecodeArgs {
     const uint16_t* lo;
     const uint32_t* lut;  // two-symbol table (hpk_code.h), step 8
     const uint32_t* lut2; // the same in the LUT2 layout (decode v12)
+    const uint32_t* lut3; // the same in the LUT3 layout (decode v28, the wave kernel)
     unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
     uint32_t in_cap, out_cap;  // blob sizes (clamped to HPK_MAX_OFFSET): larger offsets are bad
     uint32_t* err;             // sticky error flag (host-mapped): set to 1 on bad offsets

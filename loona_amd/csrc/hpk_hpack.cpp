@@ -257,14 +257,15 @@ enum Kind : uint8_t { kIndexed, kLitIncr, kSizeUpdate, kLitNever, kLitPlain };
 // the reference would have raised it.
 enum Stage : uint8_t { kStIndex = 0, kStName = 1, kStValue = 2 };
 
-struct Field {  // 40 bytes: a batch's fields are written once by the scan and read once by the apply
-    uint64_t index = 0;  // header index / name index / new table size
+struct Field {  // 32 bytes (40 until round 3): a batch's fields are written once by the scan and read once by
+                // the apply
+    uint32_t index = 0;  // header index / name index / new table size (decode_integer's <= 5 octets: < 2^29)
     Str name, value;
     int8_t err = HPK_BLK_OK;  // scan error in this field (the last field scanned)
     Kind kind = kIndexed;
     Stage err_stage = kStIndex;
 };
-static_assert(sizeof(Field) <= 40, "Field packing");
+static_assert(sizeof(Field) <= 32, "Field packing");
 
 struct Scan {  // a block's fields: pools[pool][first .. first + n) (one field pool per host thread)
     uint32_t pool = 0, first = 0, n = 0;
@@ -312,7 +313,9 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
         f.kind = (b & 128u) ? kIndexed : (b & 64u) ? kLitIncr : (b & 32u) ? kSizeUpdate : (b & 16u) ? kLitNever : kLitPlain;
         size_t c = 0;
         if (f.kind == kIndexed || f.kind == kSizeUpdate) {
-            f.err = (int8_t)decode_integer(base + pos, end - pos, f.kind == kIndexed ? 7 : 5, &f.index, &c);
+            uint64_t v = 0;
+            f.err = (int8_t)decode_integer(base + pos, end - pos, f.kind == kIndexed ? 7 : 5, &v, &c);
+            f.index = (uint32_t)v;
             pool->push_back(f);
             if (f.err) return;
             pos += c;
@@ -320,7 +323,9 @@ void scan_fields(const uint8_t* base, size_t begin, size_t end, std::vector<Fiel
         }
         // decode_literal (decoder.rs:502-527)
         const int prefix = f.kind == kLitIncr ? 6 : 4;
-        f.err = (int8_t)decode_integer(base + pos, end - pos, prefix, &f.index, &c);
+        uint64_t v = 0;
+        f.err = (int8_t)decode_integer(base + pos, end - pos, prefix, &v, &c);
+        f.index = (uint32_t)v;
         if (f.err) {
             pool->push_back(f);
             return;

@@ -97,7 +97,12 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 // s_q), kU steps between refill points, kRing input dwords per lane in s_ring and a kOS-byte
 // output buffer per lane in s_out (16-byte aligned). kDiag (diagnostic builds): per-wave counters
 // into a.dbg[wave * 16 + i] (scripts/diag_decode.py).
-template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64>
+#ifndef HPK_LONG_BODY
+#define HPK_LONG_BODY 1  // v28: body steps (no fit tests) while a literal has >= kBodyMin bits left
+#endif
+
+template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64,
+          int kTab = 2>  // kTab: the layout of s_lut (2 = LUT2, the fill kernel; 3 = LUT3, the wave kernel)
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
                                            const uint32_t* s_lut, const uint16_t* s_lo) {
@@ -319,23 +324,40 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             const uint32_t d3 = ring[((j0 + 2u) & (kRing - 1u)) * kBlock];
             const uint32_t w = __builtin_amdgcn_alignbit(d0, d1, ~X);
             const uint32_t rem = Eb - X;
-            const uint32_t e1 = s_lut[w >> (32 - HPK_LUT_BITS)];
-            bool a1, a2;
-            const uint32_t u1 = lut12(e1, rem, a1, a2);
-            bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);  // (see lit12_step)
-            const bool cont = a1 & (a2 | (e1 >= HPK_LUT2_NOTTWO));
-            const uint32_t w2 = w << u1;
-            const uint32_t rem2 = rem - u1;
-            const uint32_t e2 = s_lut[w2 >> (32 - HPK_LUT_BITS)];
-            bool b1, b2;
-            const uint32_t u2 = lut12(e2, rem2, b1, b2);
-            park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
-            b1 &= cont;
-            b2 &= cont;
+            uint32_t e1, e2, u1, u2, g1, g2;
+            bool park, prog;
+            if (HPK_LONG_BODY && rem >= kBodyMin) {
+                // body step (lit12_body): every code of the two entries ends inside the literal
+                e1 = s_lut[w >> (32 - HPK_LUT_BITS)];
+                u1 = kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
+                e2 = s_lut[(w << u1) >> (32 - HPK_LUT_BITS)];
+                u2 = kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
+                g1 = kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1);
+                g2 = kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2);
+                park = u2 == 0u;  // (> 12 bits left at e2: kBodyMin - 12)
+                prog = true;
+            } else {
+                e1 = s_lut[w >> (32 - HPK_LUT_BITS)];
+                bool a1, a2;
+                u1 = lut12<kTab>(e1, rem, a1, a2);
+                park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);  // (see lit12_step)
+                const bool cont = a1 & (a2 | lut_nottwo<kTab>(e1));
+                const uint32_t w2 = w << u1;
+                const uint32_t rem2 = rem - u1;
+                e2 = s_lut[w2 >> (32 - HPK_LUT_BITS)];
+                bool b1, b2;
+                const uint32_t v2 = lut12<kTab>(e2, rem2, b1, b2);
+                park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
+                b1 &= cont;
+                b2 &= cont;
+                g1 = (uint32_t)a1 + (uint32_t)a2;
+                g2 = (uint32_t)b1 + (uint32_t)b2;
+                u2 = cont ? v2 : 0u;
+                prog = a1 | park;
+            }
             {  // the step's (up to 4) bytes as byte stores into the lane's own buffer (bytes past the
                // ones decoded are overwritten later or never stored out; one unaligned dword store
                // instead: config 3 936.7 vs 889.7 us, gfx950 splits it)
-                const uint32_t g1 = (uint32_t)a1 + (uint32_t)a2, g2 = (uint32_t)b1 + (uint32_t)b2;
                 uint8_t* const p = obuf + (ob - lb);
                 p[0] = (uint8_t)e1;
                 p[1] = (uint8_t)(e1 >> 16);
@@ -343,13 +365,12 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 p[g1 + 1] = (uint8_t)(e2 >> 16);
                 ob += g1 + g2;
             }
-            const uint32_t xn = X + u1 + (cont ? u2 : 0u);
+            const uint32_t xn = X + u1 + u2;
             const bool cross = (xn ^ X) > 31u;
             d0 = cross ? d1 : d0;
             d1 = cross ? d2 : d1;
             d2 = cross ? d3 : d2;
             X = xn;
-            bool prog = a1 | park;
             if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup
                 const uint32_t wp = __builtin_amdgcn_alignbit(d0, d1, ~X);
                 uint32_t sy, len;

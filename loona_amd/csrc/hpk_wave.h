@@ -35,6 +35,13 @@
 #include "hpk_decode12.h"
 
 
+#ifndef HPK_BODY
+#define HPK_BODY 1  // v27: unchecked body steps + checked tails (0: v26's checked steps throughout)
+#endif
+#ifndef HPK_LUT3
+#define HPK_LUT3 1  // v28: the wave kernel's lookups in the LUT3 layout (byte-wide "bits held")
+#endif
+
 namespace hpkdec {
 
 template <int kWinB, int kImgB>
@@ -90,8 +97,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+    constexpr int kTab = HPK_LUT3 && HPK_BODY ? 3 : 2;
     for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
-        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(a.lut2)[t];
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
     if (tid < 16) s_ctr[tid] = 0;
     if (kMode == 3)
         for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
@@ -440,7 +448,70 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             bool s1 = false;
             stamp(5);
             uint32_t Lend = 0;  // the second walk's output end (bytes, image-relative)
-            if (kMode != 1) {
+            if (kMode != 1 && HPK_BODY) {
+                // v27: body steps (lit12_body, no fit tests) while a literal has >= kBodyMin bits left,
+                // slot t1's body then slot t2's; then the checked steps (lit12_step) for the two
+                // literals' last bits, t1's tail then t2's. A lane's first literal waits between the
+                // two phases as (aX, aO, aSt).
+                bool body = L.Eb - L.X >= kBodyMin;
+                uint32_t aX = L.X, aO = L.o, aSt = L.st;
+                bool aAct = L.act, onA = true;
+                for (;;) {
+                    dg_add(9, 1u);
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        if (body) lit12_body<kStore, kTab>(L, wl32, s_lut, s_lo, ol8, body);
+                        if (kMode == 6) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[0]) : "v"(L.X));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[1]) : "v"(L.o));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[2]) : "v"(L.Eb));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[3]) : "v"(L.d1));
+                            }
+                        }
+                    }
+                    if (__any(!body)) {
+                        const bool sw = !body & onA;
+                        if (sw) {  // the first literal's body is done: it waits, the second one starts
+                            aX = L.X;
+                            aO = L.o;
+                            aSt = L.st;
+                            aAct = L.act;
+                            L = N;
+                            onA = false;
+                            body = L.Eb - L.X >= kBodyMin;
+                        }
+                        if (!__any(body)) break;
+                    }
+                }
+                // tails: both literals of the lane at once, t1's from where its body stopped (restored
+                // into L), t2's (in N) from where its body stopped; a step that proves the walk has
+                // ended clears `more`, so no step is spent finding out (usually one step per tail)
+                N = L;
+                L.X = aX;
+                L.o = aO;
+                L.st = aSt;
+                L.act = aAct;
+                L.Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (aAct ? (e1.x >> 16) * 8u : 0u);
+                L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);
+                L.idx = e1.y & 0xFFFu;
+                if (aSt != HPK_OK) L.Eb = L.X;  // ended in its body (EOS / padding): no tail
+                lit12_load(L, wl32);
+                L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
+                N.more = N.Eb - N.X >= 5u;
+                while (__any(L.more | N.more)) {
+                    if (L.more) lit12_step<kStore, true, kTab, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                    if (N.more) lit12_step<kStore, true, kTab, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                }
+                // results in the v26 form: the first slot's end state saved, the second in L
+                sX = L.X;
+                sO = L.o;
+                sSt = L.st;
+                s1 = L.act;
+                L = N;
+                Lend = L.o;
+            } else if (kMode != 1) {
                 for (;;) {
                     dg_add(9, 1u);
 #pragma unroll
@@ -535,7 +606,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         static_assert(G::kWaveOff % 16 == 0, "long-phase rings");
         uint8_t* const area = smem + G::kWaveOff;
         constexpr int kLOS = 80;  // output buffer bytes per lane (the fill kernel's default geometry)
-        long_phase<512, 8, 32, 0, G::kBlock, kLOS>(a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area),
+        long_phase<512, 8, 32, 0, G::kBlock, kLOS, 64, kTab>(a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area),
                                                    area + 512 * 32 * 4,
                                                    reinterpret_cast<uint4*>(area + 512 * (32 * 4 + kLOS)), s_lut, s_lo);
     }

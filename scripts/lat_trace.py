@@ -24,9 +24,9 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     codec = HuffmanCodec(0, stream="own")
     L = _lib.lib()
-    w = synth.device_config2(codec, n=5000, seed=91)
+    w = synth.device_config2(codec, n=20000, seed=91)
     res = []
-    for n in (1000, 5000):
+    for n in (1000, 5000, 20000):
         io = w.enc_off[: n + 1].contiguous()
         blob = w.enc_blob
         oo = decode_offsets_torch(io)
@@ -46,7 +46,7 @@ def main():
             fn(*args)
             ts.append(time.perf_counter() - t0)
         assert not st.any().item()
-        res.append({"literals": n, "calls": reps, "median_us": round(statistics.median(ts) * 1e6, 1),
+        res.append({"lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")), "literals": n, "calls": reps, "median_us": round(statistics.median(ts) * 1e6, 1),
                     "p10_us": round(sorted(ts)[reps // 10] * 1e6, 1), "p90_us": round(sorted(ts)[reps * 9 // 10] * 1e6, 1)})
     for r in res:
         print(json.dumps(r), flush=True)

@@ -15,10 +15,11 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module", params=["fill", "wave"])
+@pytest.fixture(scope="module", params=["fill", "wave", "tiny"])
 def codec(request):
-    """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the v24
-    workgroup fills and the v25 wave fills), which must give identical results."""
+    """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the
+    workgroup fills, the wave fills and the lane-per-literal small-batch kernel), which must give
+    identical results."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a GPU (run with -m 'not gpu' on CPU)")
     from loona_amd import HuffmanCodec
@@ -902,3 +903,39 @@ def test_hpack_blocks_many_chunks_on_device(codec):
                     pairs.append((d, bytes.fromhex(c["wire"])))
                     want.append([(n.encode(), v.encode()) for n, v in c["headers"]])
     assert hpack.decode_blocks(pairs, codec) == want
+
+
+def test_exact_bound_regions_short_literals(codec):
+    """Short literals decoded in the fills into regions of exactly hpk_decoded_bound bytes, back to
+    back, on an unaligned output base with guard bytes: all-5-bit-code text (the decoded length
+    reaches the bound), mixed text, long codes, random bytes, EOS and bad padding. The v27 body steps
+    store unconditionally past the decoded bytes; this pins that such bytes never leave a literal's
+    own region (every neighbour is compared with the oracle, the guards must stay 0xAB)."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(5)
+    five = np.frombuffer(b"012aceiost", np.uint8)
+    text = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;,/.:ABC ", np.uint8)
+    lits = []
+    for i in range(40000):
+        k = i % 5
+        n = int(rng.integers(1, 70))
+        if k == 0:
+            lits.append(huffman_encode(rng.choice(five, n).tobytes()))
+        elif k == 1:
+            lits.append(huffman_encode(rng.choice(text, n).tobytes()))
+        elif k == 2:
+            lits.append(huffman_encode(rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+        elif k == 3:
+            lits.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        else:
+            s = bytearray(huffman_encode(rng.choice(five, n).tobytes()))
+            s[-1] ^= 0x01 if s[-1] & 1 else 0  # bad padding when the last bit was padding
+            lits.append(bytes(s))
+    blob, off = pack(lits)
+    ref = oracle_decode_batch(blob, off)
+    bound = [int(off[i + 1] - off[i]) * 8 // 5 for i in range(len(off) - 1)]
+    for shift in (0, 3):
+        got, guard = _decode_regions(codec, blob, off, bound, shift=shift)
+        compare_batches(got, ref, f"exact-bound short literals at +{shift}")
+        assert (guard == 0xAB).all()
