@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             load(L, t1);
             const uint32_t t2 = 2u * G::kBlock - 1u - t1;
             bool nv = t2 < kq;  // a second literal is waiting in N
-            load(N, t2);
+            if (!(kLate && HPK_FILL_BODY)) load(N, t2);  // (v28 loads it when it starts)
             if (kLate && HPK_FILL_BODY) {
                 // v28 (as the wave kernel, hpk_wave.h): body steps (lit12_body) while a literal has >=
                 // kBodyMin bits left, slot t1's body then slot t2's; then both tails at once with
@@ -787,7 +787,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                             aO = L.o;
                             aSt = L.st;
                             aAct = L.act;
-                            L = N;
+                            load(L, t2);
                             onA = false;
                             body = L.Eb - L.X >= kBodyMin;
                         }

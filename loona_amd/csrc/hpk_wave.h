@@ -38,6 +38,9 @@
 #ifndef HPK_BODY
 #define HPK_BODY 1  // v27: unchecked body steps + checked tails (0: v26's checked steps throughout)
 #endif
+#ifndef HPK_BODY_UNROLL
+#define HPK_BODY_UNROLL 2  // body steps between the checks for a lane whose literal's body ended
+#endif
 #ifndef HPK_LUT3
 #define HPK_LUT3 1  // v28: the wave kernel's lookups in the LUT3 layout (byte-wide "bits held")
 #endif
@@ -442,7 +445,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 lit12_load(T, wl32);
             };
             load(L, e1, t1);
-            load(N, e2, t2);
+            if (!(kMode != 1 && HPK_BODY)) load(N, e2, t2);  // (v28 loads the second literal when it starts)
             bool nv = t2 < kq;
             uint32_t sX = 0, sO = 0, sSt = 0;
             bool s1 = false;
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 for (;;) {
                     dg_add(9, 1u);
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) {
+                    for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
                         if (body) lit12_body<kStore, kTab>(L, wl32, s_lut, s_lo, ol8, body);
                         if (kMode == 6) {
 #pragma unroll
@@ -473,12 +476,13 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     }
                     if (__any(!body)) {
                         const bool sw = !body & onA;
-                        if (sw) {  // the first literal's body is done: it waits, the second one starts
+                        if (sw) {  // the first literal's body is done: it waits, the second one starts (its
+                                   // state made from the queue entry here, not carried through the loop)
                             aX = L.X;
                             aO = L.o;
                             aSt = L.st;
                             aAct = L.act;
-                            L = N;
+                            load(L, e2, t2);
                             onA = false;
                             body = L.Eb - L.X >= kBodyMin;
                         }
