@@ -127,13 +127,10 @@ int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
 
 /* Which decode kernel a context's batches use. All give identical results (the parity tests run
  * every case through each); they differ in speed by batch size. HPK_DECODE_AUTO (the default): the
- * lane-per-literal kernel with no LDS staging for batches of at most 16Ki literals (one loona
- * thread's read_headers call: latency-bound), the workgroup-fill kernel below 4M literals, the
- * wave-fill kernel from 4M on. */
+ * workgroup-fill kernel below 4M literals, the wave-fill kernel from 4M on. */
 #define HPK_DECODE_AUTO 0
 #define HPK_DECODE_FILL 1 /* workgroup fills: one fill at a time per CU, barriers between fills */
 #define HPK_DECODE_WAVE 2 /* wave fills: every wave its own fills, no barriers between them */
-#define HPK_DECODE_TINY 3 /* one lane per literal straight from global memory (small batches) */
 int hpk_ctx_set_decode_kernel(hpk_ctx* ctx, int kind);
 
 /* Read and clear the context's sticky device error flag (after HPK_ASYNC calls; synchronises the

@@ -174,11 +174,11 @@ class HuffmanCodec:
         if raw != self._bound:
             self._bind(s)
 
-    DECODE_KERNELS = {"auto": 0, "fill": 1, "wave": 2, "tiny": 3}
+    DECODE_KERNELS = {"auto": 0, "fill": 1, "wave": 2}
 
     def set_decode_kernel(self, kind: str):
-        """'auto' (default: the lane-per-literal kernel up to 16Ki literals, workgroup fills below 4M,
-        wave fills from 4M on), 'tiny', 'fill' or 'wave' (hpk_ctx_set_decode_kernel): the same
+        """'auto' (default: workgroup fills below 4M literals, wave fills from 4M on), 'fill' or
+        'wave' (hpk_ctx_set_decode_kernel): the same
         results, different speed by batch size."""
         if kind not in self.DECODE_KERNELS:
             raise ValueError(f"decode kernel {kind!r} not in {tuple(self.DECODE_KERNELS)}")

@@ -207,7 +207,7 @@ int hpk_ctx_pinned(hpk_ctx* c, size_t bytes, void** p) {
 }
 
 extern "C" int hpk_ctx_set_decode_kernel(hpk_ctx* c, int kind) {
-    if (!c || kind < HPK_DECODE_AUTO || kind > HPK_DECODE_TINY) return hpk_set_err_msg("bad decode kernel", HPK_E_INVAL);
+    if (!c || kind < HPK_DECODE_AUTO || kind > HPK_DECODE_WAVE) return hpk_set_err_msg("bad decode kernel", HPK_E_INVAL);
     c->decode_kernel = kind;
     return HPK_E_OK;
 }

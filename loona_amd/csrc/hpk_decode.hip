@@ -24,7 +24,6 @@
 // code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
 #include <stdlib.h>
 
-#include "hpk_tiny.h"
 #include "hpk_wave.h"
 
 using namespace hpkdec;
@@ -81,10 +80,6 @@ extern "C" int hpk_debug_stamps(unsigned long long* host, size_t cap_entries) {
 }
 #endif
 
-#ifndef HPK_TINY_MAX
-#define HPK_TINY_MAX 16384u  // batches of at most this many literals: hpk_decode_tiny (AUTO)
-#endif
-
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     DecodeArgs a;
     const uintptr_t ip = (uintptr_t)b.in_blob;
@@ -107,14 +102,6 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
-    const bool tiny = c->decode_kernel == HPK_DECODE_TINY || (c->decode_kernel == HPK_DECODE_AUTO && b.n <= HPK_TINY_MAX);
-    if (tiny) {  // no long-literal list, no LDS: one lane per literal (hpk_tiny.h)
-        a.long_list = nullptr;
-        a.long_min = a.long_big = 0;
-        hipLaunchKernelGGL(hpk_decode_tiny, dim3((b.n + 63u) / 64u), dim3(64), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-        return HPK_E_OK;
-    }
     uint32_t* ll = nullptr;
     int lslot = 0;
     if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
@@ -125,8 +112,11 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     if (const char* lm = getenv("HPK_LONG_MIN")) a.long_min = (uint32_t)atoi(lm);
     if (const char* lb = getenv("HPK_LONG_BIG")) a.long_big = (uint32_t)atoi(lb);
 #endif
-    // one workgroup per CU; fewer when the batch is small (>= ~64 literals per workgroup)
+    // one workgroup per CU; fewer when the batch is small (>= ~64 literals or ~32 KiB of input per
+    // workgroup: a batch of a few huge literals gets one workgroup each, hpk_huge.h)
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
+    if (blocks < ((uint64_t)b.in_cap + 32767) / 32768) blocks = ((uint64_t)b.in_cap + 32767) / 32768;
+    if (blocks > (uint64_t)b.n) blocks = (uint64_t)b.n;
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);

@@ -45,7 +45,7 @@ namespace hpkdec {
 template <int kWaves, int kW, int kO, int kQ>
 struct Geo12 : Geo7<kWaves, kW, kO, kQ, true> {
     using B = Geo7<kWaves, kW, kO, kQ, true>;
-    static constexpr int kLdsBytes = B::kCtrOff + 48;
+    static constexpr int kLdsBytes = B::kCtrOff + 48 + (int)kHugeMax * 4;  // counters, then the huge list
     static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
 };
 
@@ -294,6 +294,7 @@ __device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
 }  // namespace hpkdec
 
 #include "hpk_long.h"  // the long-literal phase
+#include "hpk_huge.h"  // the huge-literal phase
 
 namespace hpkdec {
 
@@ -337,8 +338,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     uint32_t* s_hist = reinterpret_cast<uint32_t*>(smem + G::kHistOff);
     uint32_t* s_bbase = s_hist + 64;
     // [0] fitting count, [1] lane-queue head, [2] input end of the fill, [3] output end of the
-    // fill, [4] long-queue head
+    // fill, [4] long-queue head, ... [11] huge literals listed (s_huge = s_ctr + 12; hpk_huge.h)
     uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);
+    uint32_t* s_huge = s_ctr + 12;
     for (uint32_t t = threadIdx.x; t < kLoBytes / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
     for (uint32_t t = threadIdx.x; t < (uint32_t)G::kLutBytes / 16; t += G::kBlock)
@@ -447,6 +449,13 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     // long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
     auto leave = [&](uint32_t i, uint32_t nb) {
+        if (nb >= HPK_HUGE_MIN && nb < kHugeLimit) {  // huge literals: the huge-literal phase's (hpk_huge.h)
+            const uint32_t h = atomicAdd(&s_ctr[11], 1u);
+            if (h < kHugeMax) {
+                s_huge[h] = i;
+                return;
+            }
+        }
         if (nb >= a.long_big)
             a.long_list[BA + atomicAdd(&s_ctr[6], 1u)] = i;
         else
@@ -457,6 +466,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         s_ctr[7] = 0;
         s_ctr[8] = 0;
         s_ctr[9] = 0;
+        s_ctr[11] = 0;
     }
 
     uint32_t cur = BA;
@@ -483,7 +493,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         }
         // the long-list counts before this fill (nothing changes them until the setup below): a fill
         // found bad takes back what its own literals listed
-        const uint32_t lcnt6 = s_ctr[6], lcnt7 = s_ctr[7];
+        const uint32_t lcnt6 = s_ctr[6], lcnt7 = s_ctr[7], lcnt11 = s_ctr[11];
         if (tid < 64) s_hist[tid] = 0;
         if (tid == 0) {
             s_ctr[0] = 0;
@@ -569,6 +579,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 *a.err = 1u;
                 s_ctr[6] = lcnt6;  // this fill's long literals are void too: not for the long-literal phase
                 s_ctr[7] = lcnt7;
+                s_ctr[11] = lcnt11;
             }
             break;
         }
@@ -584,6 +595,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[6] = 0;  // (this fill's entries are listed again below)
                     s_ctr[7] = 0;
+                    s_ctr[11] = 0;
                     s_ctr[10] = 0;
                 }
                 lds_barrier();
@@ -607,6 +619,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[6] = 0;
                     s_ctr[7] = 0;
+                    s_ctr[11] = 0;
                 }
                 continue;  // this fill again, from its setup (its prefetched offsets and window are still
                            // in the registers)
@@ -923,6 +936,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         lds_barrier();
         if (tid == 0) s_ctr[5] = 0;  // its claim counter
         __syncthreads();  // (every thread's list entries and stores are out)
+        static_assert(kW + kO + 12 * kQ >= huge_lds_bytes<G::kBlock>(), "huge-phase LDS");
+        huge_phase<G::kBlock, 2>(a, s_huge, min(s_ctr[11], kHugeMax), reinterpret_cast<uint32_t*>(s_in), s_lut, s_lo);
         // rings, then output buffers, then the wave queues, over the window, image, fill queue and
         // lengths (all free once the fills are done)
         constexpr int kLB = HPK_LONG_WAVES * 64;

@@ -40,6 +40,9 @@ struct DecodeArgs {
     uint32_t long_min, long_big;
 };
 
+// Huge literals (hpk_huge.h) listed per workgroup in LDS; more go to the long-literal phase.
+constexpr uint32_t kHugeMax = 16;
+
 // Per-lane state of the literal being decoded.
 struct Lit {
     uint64_t win;   // next bits, MSB-aligned (bits past the literal: whatever follows)

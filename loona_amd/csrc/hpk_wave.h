@@ -39,7 +39,7 @@
 #define HPK_BODY 1  // v27: unchecked body steps + checked tails (0: v26's checked steps throughout)
 #endif
 #ifndef HPK_BODY_UNROLL
-#define HPK_BODY_UNROLL 2  // body steps between the checks for a lane whose literal's body ended
+#define HPK_BODY_UNROLL 4  // body steps between the checks for a lane whose literal's body ended (2: config 5 +2.5 %)
 #endif
 #ifndef HPK_LUT3
 #define HPK_LUT3 1  // v28: the wave kernel's lookups in the LUT3 layout (byte-wide "bits held")
@@ -54,7 +54,7 @@ struct GeoW {
     static constexpr int kLutOff = kTabBytes;                    // T8 + LO (kTabBytes), then LUT2
     static constexpr int kWaveOff = kTabBytes + (int)HPK_LUT_SIZE * 4;
     static constexpr int kCtrOff = kWaveOff + kWaves * kWaveBytes;
-    static constexpr int kLdsBytes = kCtrOff + 64;
+    static constexpr int kLdsBytes = kCtrOff + 64 + (int)kHugeMax * 4;  // counters, then the huge list
     static constexpr int kImg = kImgB - 256;                     // usable image bytes (dummy slots after)
     static constexpr int kWinRounds = (kWinB / 16 + 63) / 64;    // window chunks per lane
     static constexpr int kFlushRounds = (kImg / 16 + 1 + 63) / 64;
@@ -62,11 +62,13 @@ struct GeoW {
     static_assert(kWinB % 16 == 0 && kImgB % 16 == 0 && kWinB < 65536 && kImgB < 131072, "entry packing");
     // the long-literal phase's rings and queues (hpk_long.h) over the wave areas after the fills
     static_assert(kWaves * kWaveBytes >= 512 * (32 * 4 + HPK_LONG_OS) + 8 * 128 * 16, "long-phase LDS");
+    static_assert(kWaves * kWaveBytes >= huge_lds_bytes<kBlock>(), "huge-phase LDS");
 };
 
 // WG counters (s_ctr): [0] bad offsets seen (waves stop at their next fill), [1] long list, front
 // (>= long_big bytes), [2] long list, back, [3] long-phase claim, [4]/[5] dense check sums, [6] the
-// dense listing found an entry it cannot list, [7] chunks of kChunk literals handed out to the waves
+// dense listing found an entry it cannot list, [7] chunks of kChunk literals handed out to the waves,
+// [8] huge literals listed (s_huge = s_ctr + 16, at most kHugeMax of them; hpk_huge.h)
 // kRank: 0 = counting sort with LDS atomics on 32 length classes of 2 bytes, 1 / 2 = ranks from
 // ballots over 16 classes of 4 bytes / 32 classes of 2 bytes (no LDS round trip)
 template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank>
@@ -97,6 +99,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     uint16_t* s_lo = reinterpret_cast<uint16_t*>(smem + kT8Bytes);
     uint32_t* s_lut = reinterpret_cast<uint32_t*>(smem + G::kLutOff);
     uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);
+    uint32_t* s_huge = s_ctr + 16;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
@@ -110,7 +113,14 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
-    auto leave = [&](uint32_t i, uint32_t nb) {  // list literal i for the long-literal phase
+    auto leave = [&](uint32_t i, uint32_t nb) {  // list literal i for the huge / long-literal phase
+        if (nb >= HPK_HUGE_MIN && nb < kHugeLimit) {
+            const uint32_t h = atomicAdd(&s_ctr[8], 1u);
+            if (h < kHugeMax) {
+                s_huge[h] = i;
+                return;
+            }
+        }
         if (nb >= a.long_big)
             a.long_list[BA + atomicAdd(&s_ctr[1], 1u)] = i;
         else
@@ -156,6 +166,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 if (tid == 0) {
                     s_ctr[1] = 0;
                     s_ctr[2] = 0;
+                    s_ctr[8] = 0;
                 }
                 __syncthreads();
             }
@@ -606,6 +617,8 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     // ---- the literals left to the long-literal phase ----
     __syncthreads();  // every wave's fills, list entries and stores are out
     const uint32_t c1 = s_ctr[1], c2 = s_ctr[2];
+    huge_phase<G::kBlock, kTab>(a, s_huge, min(s_ctr[8], kHugeMax), reinterpret_cast<uint32_t*>(smem + G::kWaveOff),
+                                s_lut, s_lo);
     if (c1 + c2) {
         static_assert(G::kWaveOff % 16 == 0, "long-phase rings");
         uint8_t* const area = smem + G::kWaveOff;

@@ -5,8 +5,7 @@
 //      end (lit12_step<.., kMore>), LUT3 and LUT2 layouts, exact-bound regions back to back, lanes in
 //      reverse order (a stray byte past a region would hit an already decoded neighbour);
 //   2. the fill kernel's protocol (hpk_decode12.h: LUT2, no second-byte offset stores);
-//   3. hpk_decode_tiny (hpk_tiny.h) lane by lane: exact-bound and below-bound regions
-//      (HPK_OUTPUT_OVERFLOW), unaligned bases, bad offsets.
+//   3. the huge-literal phase (hpk_huge.h): its per-piece functions under the workgroup's protocol.
 // Test infrastructure only (tests/test_walk_emulation.py). Exit status 0 = no mismatch.
 #include "walk.h"
 #include <cstdio>
@@ -132,81 +131,109 @@ static int run_lanes(std::mt19937_64& rng, int nlit, int maxlen) {
     return bad;
 }
 
-static int run_tiny(std::mt19937_64& rng, int nlit, int maxlen, bool below, bool badoff) {
-    auto lits = make_lits(rng, nlit, maxlen);
-    const uint32_t in_mis = rng() % 16, out_mis = rng() % 16;
-    std::vector<uint8_t> inb(16 + in_mis), outb;
-    std::vector<uint32_t> in_off(nlit + 1), out_off(nlit + 1);
-    uint32_t op = 0;
-    std::vector<uint32_t> cap(nlit);
-    for (int i = 0; i < nlit; ++i) {
-        in_off[i] = inb.size() - 16 - in_mis;
-        inb.insert(inb.end(), lits[i].begin(), lits[i].end());
-        const uint32_t bnd = lits[i].size() * 8 / 5;
-        cap[i] = below && bnd ? (uint32_t)(rng() % (bnd + 1)) : bnd;
-        out_off[i] = op;
-        op += cap[i];
-    }
-    in_off[nlit] = inb.size() - 16 - in_mis;
-    out_off[nlit] = op;
-    inb.resize(inb.size() + 64, 0x5A);
-    const int jbad = badoff ? (int)(rng() % nlit) : -1;
-    if (badoff) in_off[jbad] = in_off[jbad + 1] + 3;  // decreasing
-    outb.assign(16 + out_mis + op + 64, 0xEE);
-    std::vector<uint32_t> ol(nlit, 7);
-    std::vector<uint8_t> st(nlit, 9);
-    uint32_t err = 0;
-    DecodeArgs a = {};
-    a.in_base = inb.data() + 16;  // (the vectors' data are 16-byte aligned: new[] of >= 16 B)
-    a.in_mis = in_mis;
-    a.in_off = in_off.data();
-    a.n = nlit;
-    a.out_base = outb.data() + 16;
-    a.out_mis = out_mis;
-    a.out_off = out_off.data();
-    a.out_len = ol.data();
-    a.status = st.data();
-    a.lo = T.lo;
-    a.lut2 = T.lut2;
-    a.in_cap = in_off[nlit];
-    a.out_cap = op;
-    a.err = &err;
-    for (uint32_t b = 0; b < (uint32_t)(nlit + 63) / 64; ++b)
-        for (uint32_t l = 0; l < 64; ++l) {
-            blockIdx.x = b;
-            threadIdx.x = l;
-            hpk_decode_tiny(a);
-        }
+// The huge-literal phase (hpk_huge.h) piece by piece, with the workgroup's protocol replayed on the
+// host (pass 1 for every piece, fix rounds on a snapshot of the pieces' ends, the first terminal piece,
+// the scan, pass 2): literals of 8 KiB to 1 MiB, valid, EOS near the end or at a piece boundary, bad
+// and too-long padding, random bytes, in exact-bound regions between guard bytes.
+static int run_huge(std::mt19937_64& rng, int nlit, uint32_t lanes, long* fixes) {
+    const char* text = "abcdefghijklmnopqrstuvwxyz0123456789-_=;,/.:ABC ";
     int bad = 0;
-    for (int i = 0; i < nlit; ++i) {
-        if (badoff && i == jbad - 1) continue;  // (valid offsets, but its bytes changed with in_off[jbad])
-        if (badoff && i == jbad) {
-            if (!(st[i] == HPK_BAD_OFFSETS && ol[i] == 0 && err == 1)) {
-                if (bad < 5) printf("tiny: bad offsets of literal %d not reported\n", i);
-                ++bad;
+    for (int it = 0; it < nlit; ++it) {
+        static const uint32_t sizes[] = {8192, 9001, 16384, 65535, 65536, 65537, 100003, 262144};
+        uint32_t want = it == 0 ? (1u << 20) : sizes[rng() % 8];
+        const int kind = rng() % 7;
+        std::vector<uint8_t> enc;
+        if (kind == 6) {
+            enc.resize(want);
+            for (auto& c : enc) c = (uint8_t)rng();
+        } else {
+            std::vector<uint8_t> d(want * 8 / 5 + 16);
+            const bool five = kind == 1;
+            for (auto& c : d) c = five ? "012aceiost"[rng() % 10] : text[rng() % strlen(text)];
+            if (kind == 5)  // long codes sprinkled in (random bytes every ~300 characters)
+                for (size_t q = 0; q < d.size(); q += 200 + rng() % 200) d[q] = (uint8_t)rng();
+            enc.resize(4 * d.size() + 8);
+            size_t el = 0;
+            oracle_encode(d.data(), d.size(), enc.data(), enc.size(), &el);
+            enc.resize(std::min<size_t>(el, want));  // (cut: the tail is bad padding or a cut code)
+            if (kind == 2 && enc.size() > 8) {  // EOS near the end, or at a piece boundary
+                size_t p = rng() % 2 ? enc.size() - 6 : (enc.size() / 2) & ~(size_t)127;
+                enc[p] = enc[p + 1] = enc[p + 2] = enc[p + 3] = 0xFF;
             }
+            if (kind == 3) enc.push_back(0xFF);  // padding too long
+            if (kind == 4) enc.back() &= 0xF0;
+        }
+        const uint32_t nb = enc.size();
+        const uint32_t in_mis = rng() % 16, out_mis = rng() % 16;
+        std::vector<uint8_t> inb(16 + in_mis + nb + 64, 0x5A);
+        memcpy(inb.data() + 16 + in_mis, enc.data(), nb);
+        const uint8_t* in_base = inb.data() + 16;  // (16-byte aligned)
+        const uint32_t last16 = (in_mis + nb - 1) >> 4;
+        auto ld16 = [&](uint32_t ci) {
+            uint4 v;
+            memcpy(&v, in_base + 16 * std::min(ci, last16), 16);
+            return v;
+        };
+        const uint32_t cap = nb * 8 / 5;
+        std::vector<uint8_t> outb(16 + out_mis + cap + 64, 0xEE);
+        uint8_t* out_base = outb.data() + 16;
+        auto st8 = [&](uint32_t g, uint64_t v) {
+            if (g % 8) printf("huge: unaligned 8-byte store\n");
+            memcpy(out_base + g, &v, 8);
+        };
+        auto st1 = [&](uint32_t x, uint8_t v) { out_base[x] = v; };
+        uint32_t P, PB, OV;
+        huge_geometry(nb, lanes, P, PB, OV);
+        std::vector<uint32_t> S(P), E(P), c(P), fl(P);
+        for (uint32_t k = 0; k < P; ++k) huge_pass1<2>(ld16, T.lut2, T.lo, in_mis, nb, k, P, PB, OV, S[k], E[k], c[k], fl[k]);
+        for (int guard = 0;; ++guard) {
+            std::vector<uint32_t> from(P, kHugeNone);
+            bool any = false;
+            for (uint32_t k = 1; k < P; ++k)
+                if (!(fl[k - 1] & kHugeTerm) && E[k - 1] != kHugeNone && S[k] != E[k - 1]) from[k] = E[k - 1], any = true;
+            if (!any || guard > (int)P + 2) break;
+            for (uint32_t k = 1; k < P; ++k)
+                if (from[k] != kHugeNone) {
+                    huge_refix<2>(ld16, T.lut2, T.lo, in_mis, nb, k, P, PB, from[k], S[k], E[k], c[k], fl[k]);
+                    ++*fixes;
+                }
+        }
+        uint32_t t = kHugeNone;
+        for (uint32_t k = 0; k < P && t == kHugeNone; ++k)
+            if (fl[k] & kHugeTerm) t = k;
+        if (t == kHugeNone) {
+            printf("huge: no terminal piece (%u B)\n", nb);
+            ++bad;
             continue;
         }
-        std::vector<uint8_t> ref(lits[i].size() * 8 / 5 + 8);
-        size_t rl = 0;
-        int rs = oracle_decode(lits[i].data(), lits[i].size(), ref.data(), ref.size(), &rl);
-        const uint8_t* got = outb.data() + 16 + out_mis + out_off[i];
-        bool ok;
-        if (rl <= cap[i])
-            ok = st[i] == rs && ol[i] == rl && memcmp(got, ref.data(), rl) == 0;
-        else  // the reference's output does not fit: the walk stops at the first byte past the capacity
-            ok = st[i] == HPK_OUTPUT_OVERFLOW && ol[i] == cap[i] && memcmp(got, ref.data(), cap[i]) == 0;
-        if (!ok && bad < 5)
-            printf("tiny: literal %d (%zu B, cap %u): status %u vs %d, length %u vs %zu\n", i, lits[i].size(), cap[i],
-                   st[i], rs, ol[i], rl);
-        bad += !ok;
-    }
-    for (uint32_t j = 0; j < outb.size(); ++j)
-        if ((j < 16 + out_mis || j >= 16 + out_mis + op) && outb[j] != 0xEE) {
-            if (bad < 5) printf("tiny: guard byte %u (of %zu, regions [%u, %u)) written, below %d badoff %d\n", j,
-                                outb.size(), 16 + out_mis, 16 + out_mis + op, (int)below, (int)badoff);
-            ++bad;
+        uint32_t D = 0;
+        for (uint32_t k = 0; k <= t; ++k) {
+            huge_pass2<2>(ld16, T.lut2, T.lo, in_mis, S[k], c[k], out_mis + D, st8, st1);
+            D += c[k];
         }
+        const uint32_t olen = D, ost = fl[t] & 0xFFu;
+        std::vector<uint8_t> ref(cap + 8);
+        size_t rl = 0;
+        const int rs = oracle_decode(enc.data(), nb, ref.data(), ref.size(), &rl);
+        const bool ok = rs == (int)ost && rl == olen && memcmp(ref.data(), out_base + out_mis, rl) == 0;
+        if (!ok && bad < 5)
+            printf("huge: literal of %u B kind %d (P %u, PB %u): status %u vs %d, length %u vs %zu\n", nb, kind, P, PB, ost, rs,
+                   olen, rl);
+        bad += !ok;
+        for (uint32_t j = 0; j < outb.size(); ++j)
+            if ((j < 16 + out_mis || j >= 16 + out_mis + std::max<uint32_t>(olen, 0)) && j >= 16 + out_mis + cap &&
+                outb[j] != 0xEE) {
+                if (bad < 5) printf("huge: guard byte %u written (%u B)\n", j, nb);
+                ++bad;
+                break;
+            }
+        for (uint32_t j = 0; j < 16 + out_mis; ++j)
+            if (outb[j] != 0xEE) {
+                if (bad < 5) printf("huge: byte before the region written (%u B)\n", nb);
+                ++bad;
+                break;
+            }
+    }
     return bad;
 }
 
@@ -223,10 +250,11 @@ int main(int argc, char** argv) {
         bad += run_lanes<3, true>(rng, 3000, maxlen);
         bad += run_lanes<2, true>(rng, 3000, maxlen);
         bad += run_lanes<2, false>(rng, 3000, maxlen);
-        bad += run_tiny(rng, 3000, maxlen, false, false);
-        bad += run_tiny(rng, 3000, maxlen, true, false);
-        bad += run_tiny(rng, 500, maxlen, false, true);
     }
+    long fixes = 0;
+    bad += run_huge(rng, iters * 3, 1024, &fixes);
+    bad += run_huge(rng, iters, 64, &fixes);
+    printf("huge: %ld pieces walked again\n", fixes);
     printf("%s: %d mismatches\n", bad ? "FAIL" : "ok", bad);
     return bad != 0;
 }

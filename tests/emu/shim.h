@@ -20,6 +20,7 @@ static inline uint32_t __builtin_amdgcn_perm(uint32_t a, uint32_t b, uint32_t se
     uint32_t r=0; for(int i=0;i<4;++i){uint32_t s=(sel>>(8*i))&255; uint32_t v = s<8?bytes[s]: (s==12?0:0xFF); r|=v<<(8*i);} return r;
 }
 static inline uint32_t __clz(uint32_t x){ return x? __builtin_clz(x):32; }
+struct uint4 { uint32_t x, y, z, w; };
 struct emu_dim3 { uint32_t x = 0, y = 0, z = 0; };
 extern emu_dim3 threadIdx, blockIdx;
 static inline uint32_t hpk_bswap32(uint32_t x) { return __builtin_bswap32(x); }

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module", params=["fill", "wave", "tiny"])
+@pytest.fixture(scope="module", params=["fill", "wave"])
 def codec(request):
     """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the
     workgroup fills, the wave fills and the lane-per-literal small-batch kernel), which must give
