@@ -474,7 +474,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     dg_add(9, 1u);
 #pragma unroll
                     for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
-                        if (body) lit12_body<kStore, kTab>(L, wl32, s_lut, s_lo, ol8, body);
+                        if (body)
+                            lit12_body<kStore, kTab, (kMode >= 8 && kMode <= 10) ? kMode - 7 : 0>(L, wl32, s_lut, s_lo,
+                                                                                                   ol8, body);
                         if (kMode == 6) {
 #pragma unroll
                             for (int q = 0; q < 4; ++q) {
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             a.dbg[((uint64_t)blockIdx.x * G::kWaves + wv) * 16u + lane] = v;
         }
     }
+    signal_done(a);
 }
 
 }  // namespace hpkdec

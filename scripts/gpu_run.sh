@@ -6,6 +6,7 @@
 #   ab         dec_time.py over WLS x LIBS, ROUNDS alternating rounds (one process per run)
 #   modes      diagnostic variants of the wave kernel (libhpk_diag.so, HPK_DEBUG_MODE in MODES, default 0 1 2) on WLS
 #   pmc        FETCH_SIZE / WRITE_SIZE / SQ passes of dec_time.py on WLS (separate rocprofv3 runs)
+#   lds        LDS bank-conflict attribution: SQ counters of libhpk_diag.so modes 0 8 9 10 on config 5
 #   trace      rocprofv3 --kernel-trace --stats of a short bench run
 #   bench      bench.py (reads the pmc summaries of this OUT when present)
 # Output under gpurun_out/$TAG.
@@ -51,6 +52,15 @@ for l in open('$OUT/dec_time.jsonl'):
         python3 scripts/pmc_sq.py $OUT/pmc_sq_${wl}${sfx} $n $wl ${KERNEL:-$k} > $OUT/pmc_sq_${wl}${sfx}.json || { echo "pmc summary $wl failed"; exit 1; }
         cat $d.json $OUT/pmc_sq_${wl}${sfx}.json
       done
+    done ;;
+  lds)
+    # LDS bank-conflict attribution (libhpk_diag.so modes 8/9/10: the table reads / the window read / the
+    # byte stores of the body step issued twice) against the product's counters (mode 0), config 5
+    SQ=${SQ:-"SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_ANY"}
+    for m in ${MODES:-0 8 9 10}; do
+      HPK_LIB=loona_amd/libhpk_diag.so HPK_DEBUG_MODE=$m timeout -s KILL 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/lds_m$m -o run -- python3 scripts/dec_time.py config5 10 > $OUT/lds_m$m.log 2>&1 || { echo "lds mode $m failed"; tail $OUT/lds_m$m.log; exit 1; }
+      python3 scripts/pmc_sq.py $OUT/lds_m$m 32000000 config5 hpk_decode_wave > $OUT/lds_m$m.json || exit 1
+      echo "mode $m"; cat $OUT/lds_m$m.json
     done ;;
   trace)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu > $OUT/bench_trace.log 2>&1 || { echo "trace failed"; tail $OUT/bench_trace.log; exit 1; }

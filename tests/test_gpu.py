@@ -859,6 +859,33 @@ def test_large_literals(codec):
     assert (guard == 0xAB).all()
 
 
+def test_many_huge_literals(codec):
+    """The huge-literal phase (hpk_huge.h) with many huge literals in one workgroup's range: 64 of 8-20
+    KiB first (text, random bytes, cut mid-code), then 64k short ones, so the first workgroup lists
+    more than its 16 huge slots hold and the rest go to the long-literal phase; several huge literals
+    share a round of pieces. Against the oracle, and at exact-bound regions with guard bytes."""
+    from loona_amd import huffman_encode
+
+    rng = np.random.default_rng(88)
+    text = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_=;,/.:ABCDEFGHIJ ", np.uint8)
+    lits = []
+    for k in range(64):
+        nb = int(rng.integers(8192, 20000))
+        if k % 4 == 3:
+            lits.append(rng.integers(0, 256, nb, dtype=np.uint8).tobytes())  # EOS / padding errors early
+        else:
+            lits.append(bytes(huffman_encode(rng.choice(text, nb * 2).tobytes())[:nb]))
+    for _ in range(64000):
+        lits.append(huffman_encode(rng.choice(text, int(rng.integers(4, 30))).tobytes()))
+    blob, off = pack(lits)
+    ref = oracle_decode_batch(blob, off)
+    compare_batches(gpu_decode(codec, blob, off), ref, "many huge literals")
+    bound = [int(off[i + 1] - off[i]) * 8 // 5 for i in range(len(off) - 1)]
+    got, guard = _decode_regions(codec, blob, off, bound, shift=7)
+    compare_batches(got, ref, "many huge literals, exact-bound regions at +7")
+    assert (guard == 0xAB).all()
+
+
 def test_stream_destroyed_then_another_stream(codec):
     """a context bound to a caller-created stream A (hpk_ctx_set_stream) that the caller
     then destroys must not touch A's handle when a second stream B first uses it (the switch to
