@@ -1,7 +1,5 @@
 // hpk_ctx.hip — device context and the batch entry points of the C ABI (include/hpk.h).
 #include <stdio.h>
-
-#include <chrono>
 #include <string.h>
 #include <sys/mman.h>
 
@@ -74,11 +72,8 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     if ((e = hipMemcpy(c->d_codes, packed, sizeof(packed), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload codes", e);
     if ((e = hipHostMalloc((void**)&c->h_err, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return fail("hipHostMalloc err flag", e);
-    c->h_err[0] = 0;
-    c->h_err[1] = 0;
+    *c->h_err = 0;
     if ((e = hipHostGetDevicePointer((void**)&c->d_err, c->h_err, 0)) != hipSuccess) return fail("err flag pointer", e);
-    if ((e = hipMalloc(&c->d_wave_ctr, 4)) != hipSuccess) return fail("hipMalloc wave counter", e);
-    if ((e = hipMemset(c->d_wave_ctr, 0, 4)) != hipSuccess) return fail("clear wave counter", e);
     return c;
 }
 
@@ -154,7 +149,6 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
-    (void)hipFree(c->d_wave_ctr);
     if (c->h_pin) (void)hipHostFree(c->h_pin);
     for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
         if (c->long_ev_set[j]) (void)hipEventSynchronize(c->long_ev[j]);
@@ -373,32 +367,10 @@ static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in
         if (n == 0) return HPK_E_OK;
         if (!in_blob || !out_blob) return hpk_set_err_msg("null blob", HPK_E_INVAL);
         const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), out_off, out_len, status};
-        // a synchronous decode: its launch's last wave stores the call's number to host memory and the
-        // host spins on that word (the stream's completion wake-up took ~5 us of a small call, DESIGN
-        // §6); hipStreamSynchronize still backs it up after 20 ms (and reports a failed launch)
-        const bool spin = fn == hpk_launch_decode && !(flags & HPK_ASYNC);
-        c->spin_next = spin;
-        c->spin_used = false;
         int rc = fn(c, b);
-        c->spin_next = false;
         if (rc) return rc;
         if (!(flags & HPK_ASYNC)) {
-            bool seen = false;
-            if (c->spin_used) {
-                const volatile uint32_t* w = c->h_err + 1;
-                const auto t0 = std::chrono::steady_clock::now();
-                for (uint32_t k = 0;; ++k) {
-                    if (*w == c->done_seq) {
-                        seen = true;
-                        break;
-                    }
-                    if ((k & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
-                        break;
-                    __builtin_ia32_pause();
-                }
-                __atomic_thread_fence(__ATOMIC_ACQUIRE);
-            }
-            if (!seen) HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
             return take_err(c);
         }
         return HPK_E_OK;

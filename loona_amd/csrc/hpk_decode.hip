@@ -59,9 +59,6 @@ constexpr int kWaveWin = 3072, kWaveImg = 5888;
 #endif
 #define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, HPK_WAVE_CHUNK, HPK_WAVE_GUIDED, HPK_WAVE_RANK>
 #define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN>
-#ifndef HPK_SPIN_BLOCKS
-#define HPK_SPIN_BLOCKS 64  // synchronous calls of at most this many workgroups signal their end (signal_done)
-#endif
 
 #ifdef HPK_DIAG
 // Diagnostic build (libhpk_diag.so, `make diag`; never the product library): HPK_DEBUG_MODE selects
@@ -105,10 +102,6 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
-    a.done_ctr = nullptr;
-    a.done_flag = c->d_err + 1;
-    a.done_seq = 0;
-    a.done_blocks = 0;
     uint32_t* ll = nullptr;
     int lslot = 0;
     if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
@@ -127,12 +120,6 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
     if (blocks < 1) blocks = 1;
     const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
-    c->spin_used = c->spin_next && blocks <= HPK_SPIN_BLOCKS;
-    if (c->spin_used) {  // a small synchronous call: the last workgroup signals the host (signal_done)
-        a.done_ctr = c->d_wave_ctr;
-        a.done_seq = ++c->done_seq;
-        a.done_blocks = (uint32_t)blocks;
-    }
     bool wave = c->decode_kernel == HPK_DECODE_WAVE || (c->decode_kernel == HPK_DECODE_AUTO && b.n >= HPK_WAVE_MIN);
 #ifdef HPK_DIAG
     if (const char* wk = getenv("HPK_DECODE_KERNEL")) wave = wk[0] == 'w';  // "wave" / "fill" (A/B runs)

@@ -240,37 +240,41 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
 constexpr uint32_t kBodyMin = HPK_BODY_MIN;
 
 // kDup (diagnostic builds, LDS bank-conflict attribution): one access class of the step issued twice,
-// the second time through a volatile access whose result is discarded: 1 the two table reads, 2 the
-// window read, 3 the four byte stores (the same bytes again). The conflict cycles a variant adds over
-// the product are that class's.
+// the extra access a volatile one through an LDS-qualified pointer (a volatile access through a generic
+// pointer became a flat access, and a later plain store to the same byte let the compiler drop the
+// earlier one): 1 the two table reads, 2 the window read, 3 the four byte stores (the same bytes, the
+// duplicate first). The conflict cycles a variant adds over the product are that class's.
+#ifndef HPK_LDS_AS
+#define HPK_LDS_AS __attribute__((address_space(3)))
+#endif
 template <int kStore, int kTab = 2, int kDup = 0>
 __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                            const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, bool& body) {
     const uint32_t d3 = win32[(L.X >> 5) + 2];
-    if (kDup == 2) asm volatile("" ::"v"(reinterpret_cast<const volatile uint32_t*>(win32)[(L.X >> 5) + 2]));
+    if (kDup == 2) asm volatile("" ::"v"(((const volatile HPK_LDS_AS uint32_t*)win32)[(L.X >> 5) + 2]));
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
     const uint32_t u1 = kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
     const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
     if (kDup == 1) {
-        const volatile uint32_t* vl = lut;
+        const volatile HPK_LDS_AS uint32_t* vl = (const volatile HPK_LDS_AS uint32_t*)lut;
         asm volatile("" ::"v"(vl[w >> (32 - HPK_LUT_BITS)]));
         asm volatile("" ::"v"(vl[(w << u1) >> (32 - HPK_LUT_BITS)]));
     }
     const uint32_t u2 = kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
     const uint32_t o1 = L.o + (kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1));
     if (kStore != kNoStore) {
-        out8[L.o] = (uint8_t)e1;
-        (out8 + 1)[L.o] = (uint8_t)(e1 >> 16);
-        out8[o1] = (uint8_t)e2;
-        (out8 + 1)[o1] = (uint8_t)(e2 >> 16);
         if (kDup == 3) {
-            volatile uint8_t* v8 = out8;
+            volatile HPK_LDS_AS uint8_t* v8 = (volatile HPK_LDS_AS uint8_t*)out8;
             v8[L.o] = (uint8_t)e1;
             (v8 + 1)[L.o] = (uint8_t)(e1 >> 16);
             v8[o1] = (uint8_t)e2;
             (v8 + 1)[o1] = (uint8_t)(e2 >> 16);
         }
+        out8[L.o] = (uint8_t)e1;
+        (out8 + 1)[L.o] = (uint8_t)(e1 >> 16);
+        out8[o1] = (uint8_t)e2;
+        (out8 + 1)[o1] = (uint8_t)(e2 >> 16);
     }
     L.o = o1 + (kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2));
     const uint32_t xn = L.X + u1 + u2;
@@ -966,7 +970,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + kLB * HPK_LONG_RING * 4,
             reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo);
     }
-    signal_done(a);
 }
 
 }  // namespace hpkdec

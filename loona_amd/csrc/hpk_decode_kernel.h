@@ -38,12 +38,6 @@ struct DecodeArgs {
     // those of >= long_big bytes from the front, the others from the back
     uint32_t* long_list;
     uint32_t long_min, long_big;
-    // small synchronous calls: the launch's last workgroup to finish stores done_seq to the host-mapped
-    // done_flag (counting workgroups in done_ctr), which the host spins on instead of
-    // hipStreamSynchronize's wake-up
-    uint32_t* done_ctr;  // (nullptr: no signal)
-    uint32_t* done_flag;
-    uint32_t done_seq, done_blocks;
 };
 
 // Huge literals (hpk_huge.h) listed per workgroup in LDS; more go to the long-literal phase.
@@ -223,24 +217,6 @@ __device__ __forceinline__ void lit_bytes_to(Lit& L, const Src& src, const uint1
         L.nb -= len;
         L.rem -= len;
         L.live = L.rem != 0u;
-    }
-}
-
-// The end of a workgroup of a small synchronous call's launch (DecodeArgs::done_ctr; every thread of
-// the workgroup calls it): its stores fenced, the grid's last workgroup resets the counter and stores
-// the call's sequence number to host memory. (One atomic per wave instead: the same-address atomics
-// of a 4,096-wave grid queued for ~70 us.)
-__device__ __forceinline__ void signal_done(const DecodeArgs& a) {
-    if (!a.done_ctr) return;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0u) {
-        const uint32_t old = atomicAdd(a.done_ctr, 1u);
-        if (old + 1u == a.done_blocks) {
-            atomicExch(a.done_ctr, 0u);
-            __threadfence_system();
-            *reinterpret_cast<volatile uint32_t*>(a.done_flag) = a.done_seq;
-        }
     }
 }
 

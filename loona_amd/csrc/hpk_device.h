@@ -41,12 +41,8 @@ struct hpk_ctx {
     hipEvent_t ev_run[kMaxChunks] = {};
     hipEvent_t ev_out[kMaxChunks] = {};  // chunk j's results are in host memory
     // sticky error flag: host-mapped, written (plain store of 1) by a kernel that saw bad offsets
-    uint32_t* h_err = nullptr;  // [0] the error flag, [1] the last synchronous decode call's done word
+    uint32_t* h_err = nullptr;
     uint32_t* d_err = nullptr;
-    uint32_t* d_wave_ctr = nullptr;  // workgroups of a small synchronous decode launch that have finished
-    uint32_t done_seq = 0;           // sequence number of the last signalled call
-    bool spin_next = false;          // the next decode launch may signal its end (DecodeArgs::done_ctr)
-    bool spin_used = false;          // ... and did (a grid of at most HPK_SPIN_BLOCKS workgroups)
     // the long-literal list per stream (calls on different streams may overlap): one u32 per
     // literal of the batch, grow-only. A slot's event is recorded after the launch that used it; a
     // slot taken over from another stream (or grown) is reused only once that event has completed,

@@ -637,7 +637,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             a.dbg[((uint64_t)blockIdx.x * G::kWaves + wv) * 16u + lane] = v;
         }
     }
-    signal_done(a);
 }
 
 }  // namespace hpkdec

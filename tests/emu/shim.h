@@ -8,6 +8,7 @@
 #define __launch_bounds__(...)
 #define __shared__ static
 #define __restrict__
+#define HPK_LDS_AS
 using std::min; using std::max;
 static inline uint32_t __builtin_amdgcn_alignbit(uint32_t a, uint32_t b, uint32_t s) {
     return (uint32_t)((((uint64_t)a << 32) | b) >> (s & 31));
