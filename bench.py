@@ -489,21 +489,16 @@ def main():
                     w.drop_strings()
                     shards.append((w.enc_blob, w.enc_off))
 
-        def decode_fn(blob, off):
-            oo = decode_offsets_torch(off)
-            out = torch.empty((int(oo[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device=dev)
-            ol = torch.empty(max(off.numel() - 1, 1), dtype=torch.int32, device=dev)
-            st = torch.empty(max(off.numel() - 1, 1), dtype=torch.uint8, device=dev)
-            codec.decode_into(blob, off, out, oo, ol, st, device=True, sync=False)
-            return out, oo, ol, st
+        def decode_fn(blob, off):  # the compacted form: the owner sends its written span as it is
+            return codec.decode_compact(blob, off, sync=False)
 
-        res = shard.scatter_decode_gather(shards, decode_fn, device=dev)  # warm
+        res = shard.scatter_decode_gather(shards, decode_fn, device=dev, compacted=True)  # warm
         reps = 2
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            res = shard.scatter_decode_gather(shards, decode_fn, device=dev)
+            res = shard.scatter_decode_gather(shards, decode_fn, device=dev, compacted=True)
         torch.cuda.synchronize()
         dist.barrier()
         dt = (time.perf_counter() - t0) / reps
@@ -513,8 +508,9 @@ def main():
             e2e = {"value": round(enc_total / dt / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 3),
                    "steps": reps, "statuses_ok": bool(ok),
                    "what": "rank 0 holds the 8 shards; RCCL grouped send/recv of offsets + blob to each owner, "
-                           "device decode, the decoded bytes laid end to end on the owner, one all-reduce of the "
-                           "decoded sizes, RCCL send/recv of bytes/out_len/status back; no host copy of the data"}
+                           "device decode in the compacted form (hpk_decode_batch_compact: decoded bytes back to "
+                           "back, no gather pass), one all-reduce of the written sizes, RCCL send/recv of "
+                           "bytes/offsets/out_len/status back; no host copy of the data"}
         del res, shards
 
     line = None

@@ -115,6 +115,20 @@ int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
                      uint8_t* out_blob, size_t out_cap, const uint32_t* out_off, uint32_t* out_len,
                      uint8_t* status, int flags);
 
+/* ---- batch decode, compacted output --------------------------------------
+ * The reference returns each literal as an exact-length Vec (huffman.rs:98, 160); this form writes
+ * the decoded bytes back to back instead of into bound-sized regions: on return literal i's bytes are
+ * out_blob[out_off[i] .. out_off[i] + out_len[i]) and out_off[n] is the end of everything written.
+ * out_off (n+1 entries) is an OUTPUT here. Literals are packed in runs (a fill of the kernel at a
+ * time, literal order inside a run, runs in completion order), so out_off is not monotone; a literal
+ * of >= 64 encoded bytes keeps a region of its decoded bound, the bytes past its out_len unwritten.
+ * Device pointers only (HPK_PTR_DEVICE, optionally HPK_ASYNC); out_cap must be at least
+ * hpk_decoded_bound(in_cap) + 4 * n (HPK_E_INVAL otherwise). Statuses, errors and offsets checks
+ * as hpk_decode_batch. */
+int hpk_decode_batch_compact(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
+                             uint32_t n, uint8_t* out_blob, size_t out_cap, uint32_t* out_off, uint32_t* out_len,
+                             uint8_t* status, int flags);
+
 /* ---- batch encode --------------------------------------------------------
  * Symmetric: literal i = in_blob[in_off[i] .. in_off[i+1]) is Huffman-encoded
  * into out_blob[out_off[i] ..) with capacity out_off[i+1]-out_off[i]

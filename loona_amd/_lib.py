@@ -48,6 +48,7 @@ EXPORTS = (
     "hpk_ctx_check",
     "hpk_last_error",
     "hpk_decode_batch",
+    "hpk_decode_batch_compact",
     "hpk_encode_batch",
     "hpk_decode_batch_cpu",
     "hpk_encode_batch_cpu",
@@ -159,7 +160,7 @@ def lib() -> ctypes.CDLL:
         L.hpk_ctx_check.restype = ctypes.c_int
         L.hpk_last_error.argtypes = [ctypes.c_void_p]
         L.hpk_last_error.restype = ctypes.c_char_p
-        for fn in (L.hpk_decode_batch, L.hpk_encode_batch):
+        for fn in (L.hpk_decode_batch, L.hpk_encode_batch, L.hpk_decode_batch_compact):
             fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32,
                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_int]

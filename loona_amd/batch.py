@@ -271,6 +271,28 @@ class HuffmanCodec:
         self.decode_into(in_blob, in_off, out_blob, out_off, out_len, status, device=True, sync=sync)
         return out_blob, out_off, out_len, status
 
+    def decode_compact(self, in_blob, in_off, out_blob=None, out_off=None, out_len=None, status=None, sync=False):
+        """hpk_decode_batch_compact: torch cuda tensors -> (out_blob, out_off, out_len, status) with the
+        decoded bytes back to back (the reference's exact-length outputs, huffman.rs:98, 160): literal i
+        is out_blob[out_off[i] : out_off[i] + out_len[i]] and out_off[n] is the end of what was written.
+        out_off is an output (n + 1 entries; runs of literals in completion order, so not monotone)."""
+        import torch
+
+        n = int(in_off.shape[0]) - 1
+        dev = in_blob.device
+        need = compact_capacity(int(in_blob.numel()), n)
+        if out_blob is None:
+            out_blob = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        if out_off is None:
+            out_off = torch.empty(n + 1, dtype=torch.int32 if need < 2**31 else torch.uint32, device=dev)
+        if out_len is None:
+            out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        if status is None:
+            status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        self._call(self._L.hpk_decode_batch_compact, "hpk_decode_batch_compact", in_blob, in_off, out_blob, out_off,
+                   out_len, status, True, sync)
+        return out_blob, out_off, out_len, status
+
     def encode_device(self, in_blob, in_off, out_off=None, out_blob=None, out_len=None, status=None, sync=False):
         import torch
 
@@ -298,6 +320,11 @@ def _bound_offsets_torch(in_off, num, den, add):
     if int(out[-1].item()) >= 2**32:
         raise ValueError("bound of the shard exceeds 4 GiB")
     return out.to(torch.int32) if int(out[-1].item()) < 2**31 else out.to(torch.uint32)
+
+
+def compact_capacity(in_cap, n):
+    """Output bytes hpk_decode_batch_compact needs: hpk_decoded_bound(in_cap) + 4 n."""
+    return (8 * int(in_cap)) // 5 + 4 * int(n)
 
 
 def decode_offsets_torch(in_off):

@@ -149,6 +149,9 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
+    (void)hipFree(c->d_bound);
+    (void)hipFree(c->d_scan_tmp);
+    (void)hipFree(c->d_cursor);
     if (c->h_pin) (void)hipHostFree(c->h_pin);
     for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
         if (c->long_ev_set[j]) (void)hipEventSynchronize(c->long_ev[j]);
@@ -408,6 +411,45 @@ extern "C" int hpk_decode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_ca
                                 uint8_t* status, int flags) {
     return run_batch(hpk_launch_decode, c, in_blob, in_cap, in_off, n, out_blob, out_cap, out_off, out_len, status,
                      flags);
+}
+
+// The compacted form (include/hpk.h): the fills' bound layout made on the device by a scan of the
+// literals' 4-rounded bounds (the kernel's images keep bound-sized regions: a literal's decoded length
+// is known only once it is decoded), the output cursor zeroed, the compacted-mode fill kernel, then the
+// cursor copied to out_off[n].
+extern "C" int hpk_decode_batch_compact(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
+                                        uint32_t n, uint8_t* out_blob, size_t out_cap, uint32_t* out_off,
+                                        uint32_t* out_len, uint8_t* status, int flags) {
+    if (!c || !in_off || !out_off || (n && (!out_len || !status))) return hpk_set_err_msg("null argument", HPK_E_INVAL);
+    if (!(flags & HPK_PTR_DEVICE)) return hpk_set_err_msg("the compacted form takes device pointers only", HPK_E_INVAL);
+    if (n >= 0x7FFFFFFFu) return hpk_set_err_msg("too many literals for the compacted form", HPK_E_INVAL);
+    const uint64_t need = (uint64_t)hpk_decoded_bound(in_cap > HPK_MAX_OFFSET ? HPK_MAX_OFFSET : in_cap) + 4ull * n;
+    if (need > HPK_MAX_OFFSET) return hpk_set_err_msg("the compacted form's output would pass 4 GiB", HPK_E_INVAL);
+    if (out_cap < need) return hpk_set_err_msg("out_cap below hpk_decoded_bound(in_cap) + 4 n", HPK_E_INVAL);
+    HIP_TRY(hipSetDevice(c->device));
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(out_off, 0, 4, c->stream));
+    } else {
+        if (!in_blob || !out_blob) return hpk_set_err_msg("null blob", HPK_E_INVAL);
+        int rc;
+        if ((rc = grow((void**)&c->d_bound, &c->d_bound_cap, ((size_t)n + 1) * 4))) return rc;
+        if (!c->d_cursor) HIP_TRY(hipMalloc(&c->d_cursor, 4));
+        size_t tmp = 0;
+        if ((rc = hpk_bound_scan(c, in_off, n, c->d_bound, nullptr, &tmp))) return rc;
+        if ((rc = grow(&c->d_scan_tmp, &c->d_scan_tmp_cap, tmp))) return rc;
+        tmp = c->d_scan_tmp_cap;
+        if ((rc = hpk_bound_scan(c, in_off, n, c->d_bound, c->d_scan_tmp, &tmp))) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_cursor, 0, 4, c->stream));
+        const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), c->d_bound, out_len,
+                          status};
+        if ((rc = hpk_launch_decode_compact(c, b, out_off))) return rc;
+        HIP_TRY(hipMemcpyAsync(out_off + n, c->d_cursor, 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (!(flags & HPK_ASYNC)) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return take_err(c);
+    }
+    return HPK_E_OK;
 }
 
 extern "C" int hpk_encode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off, uint32_t n,

@@ -24,6 +24,8 @@
 // code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
 #include <stdlib.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "hpk_wave.h"
 
 using namespace hpkdec;
@@ -80,8 +82,28 @@ extern "C" int hpk_debug_stamps(unsigned long long* host, size_t cap_entries) {
 }
 #endif
 
-int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
-    DecodeArgs a;
+namespace {
+// the 4-rounded decoded bound of literal i (0 past the end), for the compacted mode's bound layout
+struct BoundOf {
+    const uint32_t* off;
+    uint32_t n;
+    __host__ __device__ uint32_t operator()(uint32_t i) const {
+        if (i >= n) return 0u;
+        const uint64_t nb = (uint64_t)(off[i + 1] - off[i]);  // (decreasing offsets: the kernel reports them)
+        const uint64_t bd = ((nb * 8u) / 5u + 3u) & ~(uint64_t)3u;
+        return bd > 0x7FFFFFFFu ? 0x7FFFFFFFu : (uint32_t)bd;
+    }
+};
+}  // namespace
+
+int hpk_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out, void* tmp, size_t* tmp_bytes) {
+    hipcub::CountingInputIterator<uint32_t> cnt(0u);
+    hipcub::TransformInputIterator<uint32_t, BoundOf, hipcub::CountingInputIterator<uint32_t>> it(cnt, BoundOf{in_off, n});
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, it, out, (int)n + 1, c->stream));
+    return HPK_E_OK;
+}
+
+static void decode_args(hpk_ctx* c, const hpk_batch& b, DecodeArgs& a) {
     const uintptr_t ip = (uintptr_t)b.in_blob;
     a.in_base = (const uint8_t*)(ip & ~(uintptr_t)15);
     a.in_mis = (uint32_t)(ip & 15);
@@ -102,6 +124,43 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
     a.err = c->d_err;
+    a.lit_out = b.out_off;
+    a.co_off = nullptr;
+    a.cursor = nullptr;
+}
+
+// one workgroup per CU; fewer when the batch is small (>= ~64 literals or ~32 KiB of input per
+// workgroup: a batch of a few huge literals gets one workgroup each, hpk_huge.h)
+static uint32_t decode_blocks(hpk_ctx* c, const hpk_batch& b) {
+    uint64_t blocks = ((uint64_t)b.n + 63) / 64;
+    if (blocks < ((uint64_t)b.in_cap + 32767) / 32768) blocks = ((uint64_t)b.in_cap + 32767) / 32768;
+    if (blocks > (uint64_t)b.n) blocks = (uint64_t)b.n;
+    if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
+    if (blocks < 1) blocks = 1;
+    return (uint32_t)blocks;
+}
+
+int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off) {
+    DecodeArgs a;
+    decode_args(c, b, a);
+    a.lit_out = co_off;
+    a.co_off = co_off;
+    a.cursor = c->d_cursor;
+    uint32_t* ll = nullptr;
+    int lslot = 0;
+    if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
+    a.long_list = ll;
+    a.long_min = HPK_LONG_MIN;
+    a.long_big = HPK_LONG_BIG;
+    hipLaunchKernelGGL((hpk_decode12<0, kWaves, kW, kO, kQ, kRefillN, true>), dim3(decode_blocks(c, b)),
+                       dim3(Geo::kBlock), 0, c->stream, a);
+    HIP_TRY(hipGetLastError());
+    return hpk_long_list_used(c, lslot);
+}
+
+int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
+    DecodeArgs a;
+    decode_args(c, b, a);
     uint32_t* ll = nullptr;
     int lslot = 0;
     if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
@@ -112,14 +171,8 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
     if (const char* lm = getenv("HPK_LONG_MIN")) a.long_min = (uint32_t)atoi(lm);
     if (const char* lb = getenv("HPK_LONG_BIG")) a.long_big = (uint32_t)atoi(lb);
 #endif
-    // one workgroup per CU; fewer when the batch is small (>= ~64 literals or ~32 KiB of input per
-    // workgroup: a batch of a few huge literals gets one workgroup each, hpk_huge.h)
-    uint64_t blocks = ((uint64_t)b.n + 63) / 64;
-    if (blocks < ((uint64_t)b.in_cap + 32767) / 32768) blocks = ((uint64_t)b.in_cap + 32767) / 32768;
-    if (blocks > (uint64_t)b.n) blocks = (uint64_t)b.n;
-    if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
-    if (blocks < 1) blocks = 1;
-    const dim3 grid((uint32_t)blocks), block(Geo::kBlock);
+    const uint32_t blocks = decode_blocks(c, b);
+    const dim3 grid(blocks), block(Geo::kBlock);
     bool wave = c->decode_kernel == HPK_DECODE_WAVE || (c->decode_kernel == HPK_DECODE_AUTO && b.n >= HPK_WAVE_MIN);
 #ifdef HPK_DIAG
     if (const char* wk = getenv("HPK_DECODE_KERNEL")) wave = wk[0] == 'w';  // "wave" / "fill" (A/B runs)

@@ -327,7 +327,13 @@ namespace hpkdec {
 // the entries, fill setup from there to the decode, -, the first fill's two setup parts, the byte
 // pass, the last write-back, setup B to the window, to the prefetch, to the write-back issue),
 // 4 checked stores (g_chk), 5 product + per-wave counters of the long-literal phase in a.dbg.
-template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN>
+// kCompact: the compacted-output mode (hpk_decode_batch_compact): a.out_off is the library's own
+// bound layout of the fills' images; every fill, once decoded, takes its decoded total from the device
+// cursor and writes its literals' bytes there back to back (compact_flush), with their offsets in
+// a.co_off; a listed (huge / long) literal takes its decoded bound when its phase starts it (a
+// literal can be listed twice: a fill whose setup is redone lists its long literals again).
+constexpr uint32_t kListed = 0xFFFFFFFFu;  // (kCompact) s_lenst mark of a literal listed, not decoded by its fill
+template <int kMode, int kWaves, int kW, int kO, int kQ, int kRefillN, bool kCompact = false>
 __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     using G = Geo12<kWaves, kW, kO, kQ>;
     constexpr int R = G::kMetaRounds, S = G::kStageRounds;
@@ -339,7 +345,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     // HPK_FLUSH_LOOP: the previous fill's last S write-back rounds are read into the window-prefetch
     // registers (free once the window is in LDS) and stored from the lane loop, before the window's
     // prefetch loads reuse those registers
-    constexpr int kFD = kPfLoop ? (HPK_FLUSH_LOOP < S ? HPK_FLUSH_LOOP : S) : 0;
+    constexpr int kFD = kPfLoop && !kCompact ? (HPK_FLUSH_LOOP < S ? HPK_FLUSH_LOOP : S) : 0;
     // groups of one fill prefetch: a round of offsets each, the deferred write-back rounds, the window
     constexpr int kPfN = R + kFD + 1;
     // kPred: the image's last 256 bytes are the lanes' dummy slots (one dword apart), not output
@@ -467,6 +473,87 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
     };
+    // kCompact: the decoded fill [fcur, fcur + fk) written back compacted (the fill's image at ob16c,
+    // out_base-relative; its literals' image offsets read again from the bound layout): a block scan of
+    // the lengths in literal
+    // order, ONE cursor add for the fill's total, then every thread copies its own literals from the
+    // image to their places (a few bytes to the first dword boundary, dword stores assembled from the
+    // image's dwords by alignbyte, the last bytes); lengths, statuses and offsets. (A gather of whole
+    // 16-byte destination chunks, each finding its literal by binary search and reading the image byte
+    // by byte, measured 2.47 ms per config-5 launch.) Listed literals (kListed) are 0 bytes here.
+#ifndef HPK_COMPACT_STATIC
+#define HPK_COMPACT_STATIC 0
+#endif
+#ifndef HPK_COMPACT_NOCOPY
+#define HPK_COMPACT_NOCOPY 0  // (measurement only: no copy, no lengths)
+#endif
+    [[maybe_unused]] uint32_t wg_cur = BA < BB ? a.out_off[BA] : 0u;  // (HPK_COMPACT_STATIC only)
+    auto compact_flush = [&](uint32_t fcur, uint32_t fk, uint32_t ob16c) {
+        uint32_t io[R];  // (loads in flight under the scan)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            io[r] = a.out_off[fcur + min(t, fk - 1u)] + a.out_mis - ob16c;
+        }
+        lds_barrier();  // every length and status of the fill is in s_lenst
+        const uint32_t wv = tid >> 6;
+        uint32_t len[R], lst[R], exs[R];
+        uint32_t carry = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            lst[r] = t < fk ? s_lenst[t] : kListed;
+            len[r] = lst[r] == kListed ? 0u : lst[r] & 0xFFFFFFu;
+            uint32_t x = len[r];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= (uint32_t)d) x += y;
+            }
+            if (lane == 63u) s_hist[wv] = x;
+            lds_barrier();
+            uint32_t pre = 0, tot = 0;
+            for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) {
+                const uint32_t v = s_hist[q];
+                pre += q < wv ? v : 0u;
+                tot += v;
+            }
+            exs[r] = carry + pre + x - len[r];
+            carry += tot;
+            lds_barrier();  // (s_hist again in the next round)
+        }
+#if HPK_COMPACT_STATIC  // (measurement only: the workgroup's fills packed into its range's bound span, no cursor)
+        const uint32_t base = wg_cur;
+        wg_cur += carry;
+        lds_barrier();
+#else
+        if (tid == 0) s_hist[32] = atomicAdd(a.cursor, carry);
+        lds_barrier();
+        const uint32_t base = s_hist[32];
+#endif
+        const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_out);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            if (t < fk && lst[r] != kListed && !HPK_COMPACT_NOCOPY) {
+                a.co_off[fcur + t] = base + exs[r];
+                a.out_len[fcur + t] = len[r];
+                a.status[fcur + t] = (uint8_t)(lst[r] >> 24);
+                uint32_t x = a.out_mis + base + exs[r], sp = io[r];
+                const uint32_t e = x + len[r];
+                for (; x < e && (x & 3u); ++x, ++sp) a.out_base[x] = s_out[sp];
+                if (x + 4u <= e) {
+                    uint32_t lo = img32[sp >> 2];
+                    for (; x + 4u <= e; x += 4u, sp += 4u) {
+                        const uint32_t hi = img32[(sp >> 2) + 1u];
+                        *reinterpret_cast<uint32_t*>(a.out_base + x) = __builtin_amdgcn_alignbyte(hi, lo, sp & 3u);
+                        lo = hi;
+                    }
+                }
+                for (; x < e; ++x, ++sp) a.out_base[x] = s_out[sp];
+            }
+        }
+    };
     // long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])
     auto leave = [&](uint32_t i, uint32_t nb) {
@@ -553,6 +640,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
                 if (fast && nbytes >= a.long_min) {  // the long-literal phase's (not queued here)
                     leave(cur + t, nbytes);
+                    if (kCompact) s_lenst[t] = kListed;
                 } else {
                     const uint32_t bk = lpt_bucket(nbytes);
                     pos[r] = (bk << 16) | atomicAdd(&s_hist[bk], 1u);
@@ -657,6 +745,11 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             if (tid == 0 && !left) {
                 const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), last16 * 4 + 3};
                 uint8_t* dst = a.out_base + gout;
+                if (kCompact) {  // (a region below the bound cannot happen here: the library makes them)
+                    const uint32_t nb = a.in_off[cur + 1] - a.in_off[cur];
+                    a.co_off[cur] = atomicAdd(a.cursor, (nb * 8u) / 5u);
+                    dst = a.out_base + a.out_mis + a.co_off[cur];
+                }
                 Lit L = {};
                 lit_bytes_to(L, g, s_lo, [&](uint32_t j, uint8_t v) { dst[j] = v; },
                              a.out_off[cur + 1] - a.out_off[cur], gin, a.in_off[cur + 1] + a.in_mis - gin);
@@ -756,10 +849,12 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             else
                 flush(pcur, pk, pG0, pG1);
         }
-        pk = k;
-        pcur = cur;
-        pG0 = gout;
-        pG1 = gout_next;
+        if (!kCompact) {  // (the compacted mode writes each fill back once it is decoded: compact_flush)
+            pk = k;
+            pcur = cur;
+            pG0 = gout;
+            pG1 = gout_next;
+        }
         if (kMode == 3) t_sb3 += __builtin_amdgcn_s_memtime() - tb0;  // (mode 3: + write-back issued)
         lds_barrier();
         unsigned long long td0 = 0;
@@ -925,6 +1020,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             }
         }
         if (kMode == 3) t_byte += __builtin_amdgcn_s_memtime() - tq0;
+        if (kCompact) compact_flush(cur, k, ob16);
         cur = cur_next;
         gin = gin_next;
         gout = gout_next;
@@ -966,7 +1062,8 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
                           kW % 16 == 0 && kLQ % 16 == 0 && G::kHistOff == G::kInOff + kW + kO + 12 * kQ,
                       "long-phase LDS");
-        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM>(
+        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, 2,
+                   kCompact>(
             a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + kLB * HPK_LONG_RING * 4,
             reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo);
     }

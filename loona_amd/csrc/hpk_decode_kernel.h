@@ -38,6 +38,13 @@ struct DecodeArgs {
     // those of >= long_big bytes from the front, the others from the back
     uint32_t* long_list;
     uint32_t long_min, long_big;
+    // where the long- and huge-literal phases write literal i: lit_out[i] (out_off; in the compacted
+    // mode the compacted offsets co_off, allocated when the literal is listed)
+    const uint32_t* lit_out;
+    // compacted mode (hpk_decode_batch_compact): co_off[i] = where literal i's bytes went, allocated from
+    // the device cursor *cursor per fill (fill literals) or per listed literal (its decoded bound)
+    uint32_t* co_off;
+    uint32_t* cursor;
 };
 
 // Huge literals (hpk_huge.h) listed per workgroup in LDS; more go to the long-literal phase.

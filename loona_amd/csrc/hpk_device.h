@@ -55,6 +55,13 @@ struct hpk_ctx {
     size_t long_list_cap[kLongSlots] = {};
     int long_next = 0;
     bool long_multi = false;  // more than one stream has used the context: slots carry events
+    // the compacted mode (hpk_decode_batch_compact): the fills' bound layout, the scan's scratch and the
+    // output cursor, grow-only
+    uint32_t* d_bound = nullptr;
+    size_t d_bound_cap = 0;
+    void* d_scan_tmp = nullptr;
+    size_t d_scan_tmp_cap = 0;
+    uint32_t* d_cursor = nullptr;
 };
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on
@@ -87,6 +94,12 @@ int hpk_set_err_msg(const char* what, int code);
     } while (0)
 
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b);
+// The compacted mode: b.out_off is the bound layout made by hpk_bound_scan, co_off the caller's output
+// offsets, c->d_cursor the (zeroed) output cursor.
+int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off);
+// out[i] = sum over j < i of the 4-rounded decoded bound of literal j (n + 1 entries), on the ctx
+// stream; tmp == nullptr: *tmp_bytes = the scratch it needs.
+int hpk_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out, void* tmp, size_t* tmp_bytes);
 int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b);
 
 __device__ __forceinline__ uint32_t hpk_bswap32(uint32_t x) { return __builtin_bswap32(x); }

@@ -243,7 +243,7 @@ namespace hpkdec {
 // bounds, regions >= the decoded bound) and a scratch area of LDS (kHugeLds bytes, 16-byte aligned).
 template <int kBlock>
 constexpr int huge_lds_bytes() {
-    return 3 * kBlock * 4 + (4 * kHugeMax + 4 + 16) * 4;
+    return 3 * kBlock * 4 + (5 * kHugeMax + 4 + 16) * 4;
 }
 
 template <int kBlock, int kTab>
@@ -258,7 +258,8 @@ __device__ void huge_phase(const DecodeArgs& a, const uint32_t* s_list, uint32_t
     uint32_t* const jb = jl + kHugeMax;
     uint32_t* const jp = jb + kHugeMax;
     uint32_t* const jt = jp + kHugeMax;
-    uint32_t* const jm = jt + kHugeMax;      // [0] jobs, [1] next list entry, [2] lanes used, [3..4] fix flags
+    uint32_t* const jo = jt + kHugeMax;      // output offset (out_base-relative, before out_mis)
+    uint32_t* const jm = jo + kHugeMax;      // [0] jobs, [1] next list entry, [2] lanes used, [3..4] fix flags
     uint32_t* const wt = jm + 4;             // wave totals of the scan
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1u) >> 4 : 0u;
@@ -278,6 +279,9 @@ __device__ void huge_phase(const DecodeArgs& a, const uint32_t* s_list, uint32_t
                 huge_geometry(nb, kBlock, P, PB, OV);
                 if (used + P > (uint32_t)kBlock) break;
                 jl[nj] = i;
+                // (the compacted mode, a.cursor set: the literal's decoded bound from the cursor, now)
+                jo[nj] = a.cursor ? atomicAdd(a.cursor, (nb * 8u) / 5u) : a.lit_out[i];
+                if (a.cursor) a.co_off[i] = jo[nj];
                 jb[nj] = used;
                 jp[nj] = P;
                 jt[nj] = kHugeNone;
@@ -295,7 +299,7 @@ __device__ void huge_phase(const DecodeArgs& a, const uint32_t* s_list, uint32_t
         const bool on = tid < used;
         uint32_t j = 0;
         for (uint32_t q = 1; q < nj; ++q) j = jb[q] <= tid ? q : j;
-        const uint32_t i = jl[j], base = jb[j];
+        const uint32_t i = jl[j], base = jb[j], obase = jo[j];
         const uint32_t k = tid - base;
         const uint32_t p0 = a.in_off[i], nbytes = a.in_off[i + 1] - p0;
         const uint32_t lbyte = p0 + a.in_mis;
@@ -349,7 +353,7 @@ __device__ void huge_phase(const DecodeArgs& a, const uint32_t* s_list, uint32_t
         __syncthreads();
         if (live) {
             const uint32_t D = ex - mX[base];
-            huge_pass2<kTab>(ld16, s_lut, s_lo, lbyte, S, c, a.out_off[i] + a.out_mis + D, st8, st1);
+            huge_pass2<kTab>(ld16, s_lut, s_lo, lbyte, S, c, obase + a.out_mis + D, st8, st1);
             if (k == t) {
                 a.out_len[i] = D + c;
                 a.status[i] = (uint8_t)(fl & 0xFFu);

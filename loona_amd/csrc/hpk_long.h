@@ -102,7 +102,8 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 #endif
 
 template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64,
-          int kTab = 2>  // kTab: the layout of s_lut (2 = LUT2, the fill kernel; 3 = LUT3, the wave kernel)
+          int kTab = 2,            // kTab: the layout of s_lut (2 = LUT2, the fill kernel; 3 = LUT3, the wave kernel)
+          bool kCompact = false>   // the compacted mode: a claim takes its literals' decoded bounds from a.cursor
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
                                            const uint32_t* s_lut, const uint16_t* s_lo) {
@@ -287,7 +288,23 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             // straight-line loads (no branch around them): a load under a branch leaves the compiler
             // unsure whether its register is still pending, and it then waits for all memory
             // operations (the refill loads included) before the steps reuse the register
-            const uint4 li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.out_off[i]);
+            uint4 li;
+            if (kCompact) {  // the claim's literals' decoded bounds: one cursor add per claim, offsets to co_off
+                li = make_uint4(i, a.in_off[i], a.in_off[i + 1], 0u);
+                const uint32_t bd = ok ? ((li.z - li.y) * 8u) / 5u : 0u;
+                uint32_t x = bd;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(x, d);
+                    if (lane >= (uint32_t)d) x += y;
+                }
+                uint32_t cb = 0;
+                if (lane == 63u) cb = atomicAdd(a.cursor, x);
+                li.w = (uint32_t)__builtin_amdgcn_readlane((int)cb, 63) + x - bd;
+                if (ok) a.co_off[i] = li.w;
+            } else {
+                li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.lit_out[i]);
+            }
             const uint64_t lm = __ballot(ok);
             const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
             if (ok) sq[wv][(qt + lr) % kQ] = li;

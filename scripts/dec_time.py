@@ -23,11 +23,15 @@ def main():
             "c2_4m": lambda c: synth.device_config2(c, n=4_000_000),
             "config5": lambda c: synth.device_config5_shard(c, 0)}
     w = gens[wl](codec)
-    doff = decode_offsets_torch(w.enc_off)
-    out = torch.empty(int(doff[-1].item()) + 16, dtype=torch.uint8, device="cuda")
-    ol = torch.empty(w.n, dtype=torch.int32, device="cuda")
-    st = torch.empty(w.n, dtype=torch.uint8, device="cuda")
-    codec.decode_into(w.enc_blob, w.enc_off, out, doff, ol, st, device=True)  # binds the stream, checks args
+    compact = os.environ.get("HPK_COMPACT", "0") == "1"  # hpk_decode_batch_compact instead
+    if compact:
+        out, doff, ol, st = codec.decode_compact(w.enc_blob, w.enc_off)
+    else:
+        doff = decode_offsets_torch(w.enc_off)
+        out = torch.empty(int(doff[-1].item()) + 16, dtype=torch.uint8, device="cuda")
+        ol = torch.empty(w.n, dtype=torch.int32, device="cuda")
+        st = torch.empty(w.n, dtype=torch.uint8, device="cuda")
+        codec.decode_into(w.enc_blob, w.enc_off, out, doff, ol, st, device=True)  # binds the stream, checks args
     torch.cuda.synchronize()
     if os.environ.get("HPK_DEBUG_MODE", "0") in ("0", "3", "4", "5"):
         synth.check_decoded(w, out, doff, ol, st)
@@ -38,7 +42,7 @@ def main():
     args = (codec._h, ctypes.c_void_p(w.enc_blob.data_ptr()), w.enc_blob.numel(), ctypes.c_void_p(w.enc_off.data_ptr()),
             ctypes.c_uint32(w.n), ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.c_void_p(doff.data_ptr()),
             ctypes.c_void_p(ol.data_ptr()), ctypes.c_void_p(st.data_ptr()), _lib.HPK_PTR_DEVICE | _lib.HPK_ASYNC)
-    fn = L.hpk_decode_batch
+    fn = L.hpk_decode_batch_compact if compact else L.hpk_decode_batch
     run = lambda: fn(*args)  # noqa: E731
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,7 +59,8 @@ def main():
                       "lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")),
                       "debug_mode": os.environ.get("HPK_DEBUG_MODE", "0"),
                       "kernel": os.environ.get("HPK_DECODE_KERNEL", "auto"),
-                      "wave_variant": os.environ.get("HPK_WAVE_VARIANT")}), flush=True)
+                      "wave_variant": os.environ.get("HPK_WAVE_VARIANT"), "compact": compact,
+                      "written_bytes": int(doff[-1].item()) & 0xFFFFFFFF if compact else None}), flush=True)
 
 
 if __name__ == "__main__":

@@ -15,17 +15,19 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module", params=["fill", "wave"])
+@pytest.fixture(scope="module", params=["fill", "wave", "compact"])
 def codec(request):
     """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the
-    workgroup fills, the wave fills and the lane-per-literal small-batch kernel), which must give
-    identical results."""
+    workgroup fills and the wave fills) and in the compacted-output form (hpk_decode_batch_compact,
+    through gpu_decode / _device_decode; tests that pass their own output regions run the fill kernel
+    there), which must all give identical results."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a GPU (run with -m 'not gpu' on CPU)")
     from loona_amd import HuffmanCodec
 
     c = HuffmanCodec(0, stream=torch.cuda.current_stream())
-    c.set_decode_kernel(request.param)
+    c.set_decode_kernel("fill" if request.param == "compact" else request.param)
+    c.compact = request.param == "compact"
     yield c
     c.close()
 
@@ -47,10 +49,32 @@ def gpu_decode(codec, blob, off, shift=0):
     else:
         dblob = to_dev(blob if blob.size else np.zeros(1, np.uint8))
     doff = to_dev(np.asarray(off, np.int64).astype(np.int32))
-    out, oo, ol, st = codec.decode_device(dblob, doff, sync=True)
+    if getattr(codec, "compact", False):
+        out, oo, ol, st = codec.decode_compact(dblob, doff, sync=True)
+        _check_compact(out, oo, ol, n)
+    else:
+        out, oo, ol, st = codec.decode_device(dblob, doff, sync=True)
     torch.cuda.synchronize()
     return (out.cpu().numpy(), oo.cpu().numpy().astype(np.uint32), ol[:n].cpu().numpy().astype(np.uint32),
             st[:n].cpu().numpy())
+
+
+def _check_compact(out, oo, ol, n):
+    """The compacted form's layout: literals' byte ranges disjoint and inside out_off[n], which is at
+    most the output capacity."""
+    if n == 0:
+        assert int(oo[0].item()) == 0
+        return
+    o = oo.to(torch.int64) & 0xFFFFFFFF
+    ln = ol[:n].to(torch.int64)
+    end = int(o[n].item())
+    assert end <= out.numel()
+    assert bool(((o[:n] + ln) <= end).all().item())
+    nz = ln > 0  # (an empty literal may share its start with its neighbour)
+    s, e = o[:n][nz], (o[:n] + ln)[nz]
+    order = torch.argsort(s)
+    s, e = s[order], e[order]
+    assert bool((s[1:] >= e[:-1]).all().item()), "compacted literals overlap"
 
 
 def gpu_encode(codec, blob, off):
@@ -642,14 +666,25 @@ def test_bad_offsets_with_long_literals_in_the_fill(codec):
 
 
 def _prefix_host(out, oo, ol, st, k):
-    """The first k literals of a device decode as numpy (out_blob, out_off, out_len, status)."""
-    end = int(oo[k].item()) & 0xFFFFFFFF
-    return (out[:end].cpu().numpy(), oo[: k + 1].cpu().numpy().view(np.uint32).copy(),
-            ol[:k].cpu().numpy().view(np.uint32).copy(), st[:k].cpu().numpy())
+    """The first k literals of a device decode as numpy (out_blob, out_off, out_len, status); their
+    bytes gathered on the device first (the compacted form's offsets are not monotone)."""
+    from loona_amd import synth
+
+    got = synth.gather_output(out, oo, ol, 0, k)
+    ln = ol[:k].cpu().numpy().view(np.uint32).astype(np.int64)
+    offs = np.zeros(k + 1, np.int64)
+    np.cumsum(ln, out=offs[1:])
+    return (got.cpu().numpy() if got.numel() else np.zeros(1, np.uint8), offs.astype(np.uint32),
+            ln.astype(np.uint32), st[:k].cpu().numpy())
 
 
 def _device_decode(codec, w):
     from loona_amd.batch import decode_offsets_torch
+
+    if getattr(codec, "compact", False):
+        out, oo, ol, st = codec.decode_compact(w.enc_blob, w.enc_off, sync=True)
+        _check_compact(out, oo, ol, w.n)
+        return out, oo, ol, st
 
     oo = decode_offsets_torch(w.enc_off)
     out = torch.empty((int(oo[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device="cuda")
@@ -781,6 +816,8 @@ def test_scatter_decode_gather_device_world1(codec):
             shards.append((to_dev(sb if sb.size else np.zeros(1, np.uint8)), to_dev(so.view(np.int32))))
 
         def decode_fn(blob, off):
+            if codec.compact:  # the compacted form: the owner's written span travels as it is
+                return codec.decode_compact(blob, off, sync=False)
             oo = decode_offsets_torch(off)
             out = torch.empty((int(oo[-1].item()) & 0xFFFFFFFF) + 16, dtype=torch.uint8, device="cuda")
             ol = torch.empty(max(off.numel() - 1, 1), dtype=torch.int32, device="cuda")
@@ -788,7 +825,7 @@ def test_scatter_decode_gather_device_world1(codec):
             codec.decode_into(blob, off, out, oo, ol, st, device=True, sync=False)
             return out, oo, ol, st
 
-        res = shard.scatter_decode_gather(shards, decode_fn, device="cuda")
+        res = shard.scatter_decode_gather(shards, decode_fn, device="cuda", compacted=codec.compact)
         torch.cuda.synchronize()
         for r, (cb, coff, ol, st) in enumerate(res):  # each shard's decoded bytes laid end to end
             lo, hi = int(b[r]), int(b[r + 1])

@@ -81,7 +81,28 @@ def _cpu_decode(b, o):
             torch.from_numpy(st))
 
 
-def _worker(rank, world, port, n, seed, nshards, q):
+def _cpu_decode_compacted(b, o):
+    """A stand-in for the compacted form on CPU tensors: the CPU batch decode, then the literals' bytes
+    packed back to back in runs of 7 taken in reverse order (as the device's completion order would
+    scatter them), out_off = each literal's start, out_off[m] = the span written."""
+    import torch
+
+    ob, oo, ol, st = decode_batch_cpu(b.numpy(), o.numpy().view(np.uint32), nthreads=2)
+    m = len(ol)
+    starts = np.zeros(m + 1, np.int64)
+    out = np.zeros(max(int(ol.sum()), 1), np.uint8)
+    pos = 0
+    for r0 in reversed(range(0, m, 7)):
+        for i in range(r0, min(m, r0 + 7)):
+            starts[i] = pos
+            out[pos : pos + int(ol[i])] = ob[int(oo[i]) : int(oo[i]) + int(ol[i])]
+            pos += int(ol[i])
+    starts[m] = pos
+    return (torch.from_numpy(out), torch.from_numpy(starts.astype(np.int32)), torch.from_numpy(ol.view(np.int32)),
+            torch.from_numpy(st))
+
+
+def _worker(rank, world, port, n, seed, nshards, q, compacted=False):
     import torch
     import torch.distributed as dist
 
@@ -97,13 +118,39 @@ def _worker(rank, world, port, n, seed, nshards, q):
             for r in range(nshards):
                 sb, so = shard.shard(blob, off, int(b[r]), int(b[r + 1]))
                 shards.append((torch.from_numpy(np.ascontiguousarray(sb)), torch.from_numpy(so.view(np.int32))))
-        res = shard.scatter_decode_gather(shards, _cpu_decode)
+        res = shard.scatter_decode_gather(shards, _cpu_decode_compacted if compacted else _cpu_decode,
+                                          compacted=compacted)
         if rank == 0:
             q.put([tuple(x.numpy() for x in r) for r in res])
         else:
             assert res is None
     finally:
         dist.destroy_process_group()
+
+
+def test_scatter_decode_gather_gloo_compacted():
+    """The same over gloo with a compacted decode (scatter_decode_gather(compacted=True)): each owner's
+    written span and its per-literal starts travel as they are; root's results equal the oracle's."""
+    import torch.multiprocessing as mp
+
+    n, seed, world, nshards = 12000, 6, 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, nshards, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    blob, off = _lits(n, seed)
+    b = shard.balanced_ranges(off, nshards)
+    for r, (cb, coff, ol, st) in enumerate(res):
+        assert int(coff[-1]) == cb.size
+        sb, so = shard.shard(blob, off, int(b[r]), int(b[r + 1]))
+        got = (cb if cb.size else np.zeros(1, np.uint8), coff.astype(np.uint32), ol.view(np.uint32), st)
+        compare_batches(got, oracle_decode_batch(sb, so), f"compacted shard {r}")
 
 
 @pytest.mark.parametrize("world,nshards", [(2, 5), (3, 3)])
