@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 encode/decode side measurement")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 captured-HEADERS side measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the scatter+decode+gather leg (N > 1)")
+    ap.add_argument("--no-compact", action="store_true", help="skip the compacted-output side measurement")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every CPU of this process's affinity mask, capped at the GPU's host-CPU share (16)")
     ap.add_argument("--pmc-dir", default=os.path.join(REPO, "profiles"))
@@ -247,6 +248,43 @@ def cuda_time(fn, reps, stream):
     e1.record(stream)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def run_compact(codec, w, stream, pmc_dir, reps=10):
+    """The compacted-output form (hpk_decode_batch_compact) on one config-5 shard: every decoded byte
+    checked, then `reps` back-to-back launches timed with HIP events on the codec's stream; the span it
+    wrote and, when a same-source PMC summary of it exists (gpu_run.sh pmc with HPK_COMPACT=1), its HBM
+    writes against the algorithmic ones (decoded bytes + out_off + out_len + status)."""
+    import torch
+
+    from loona_amd import synth
+
+    out, oo, ol, st = codec.decode_compact(w.enc_blob, w.enc_off, sync=True)
+    synth.check_decoded(w, out, oo, ol, st)
+    written = int(oo[w.n].item()) & 0xFFFFFFFF
+    for _ in range(2):
+        codec.decode_compact(w.enc_blob, w.enc_off, out, oo, ol, st)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        codec.decode_compact(w.enc_blob, w.enc_off, out, oo, ol, st)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    res = {"literals": w.n, "encoded_bytes": w.enc_bytes, "decoded_bytes": w.dec_bytes, "written_span": written,
+           "avg_call_us": round(us, 1), "calls": reps,
+           "note": "one config-5 shard; a call = the bound-layout scan + the compacted-mode fill kernel + the "
+                   "cursor copy; every byte checked"}
+    p = os.path.join(pmc_dir, "pmc_compact_config5.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        if d.get("src_sha16") == source_hash():
+            algo_w = w.dec_bytes + 9 * w.n
+            res["pmc_write_bytes"] = d["write_bytes_per_launch"]
+            res["write_algorithmic"] = algo_w
+            res["write_vs_algorithmic"] = round(d["write_bytes_per_launch"] / algo_w, 4)
+    return res
 
 
 def run_config3(codec, stream, dev, reps=10):
@@ -603,7 +641,10 @@ def main():
         if e2e is not None:
             line["e2e_scatter_decode_gather"] = e2e
 
-    # ---- config-2 side measurement and CPU baselines (rank 0) ----
+    # ---- the compacted form, config-2 side measurement and CPU baselines (rank 0) ----
+    if rank == 0 and args.workload == "config5" and not args.no_compact:
+        line["config5_compact"] = run_compact(codec, units[0][0], stream, args.pmc_dir)
+        torch.cuda.empty_cache()
     if rank == 0 and args.workload == "config5" and not args.no_config2:
         del units, by_shard
         torch.cuda.empty_cache()

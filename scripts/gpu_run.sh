@@ -5,7 +5,8 @@
 #   smoke      __graft_entry__.smoke()
 #   ab         dec_time.py over WLS x LIBS, ROUNDS alternating rounds (one process per run)
 #   modes      diagnostic variants of the wave kernel (libhpk_diag.so, HPK_DEBUG_MODE in MODES, default 0 1 2) on WLS
-#   pmc        FETCH_SIZE / WRITE_SIZE / SQ passes of dec_time.py on WLS (separate rocprofv3 runs)
+#   pmc        FETCH_SIZE / WRITE_SIZE / SQ passes of dec_time.py on WLS (separate rocprofv3 runs; with
+#              HPK_COMPACT=1 the compacted form, summaries named pmc_compact_*)
 #   lds        LDS bank-conflict attribution: SQ counters of libhpk_diag.so modes 0 8 9 10 on config 5
 #   trace      rocprofv3 --kernel-trace --stats of a short bench run
 #   bench      bench.py (reads the pmc summaries of this OUT when present)
@@ -44,13 +45,13 @@ for l in open('$OUT/dec_time.jsonl'):
     for wl in $WLS; do
       k=$(kernel_of $wl); n=$(lits_of $wl)
       for lib in $LIBS; do
-        sfx=${lib#libhpk}; sfx=${sfx%.so}; d=$OUT/pmc_${wl}${sfx}
+        sfx=${lib#libhpk}; sfx=${sfx%.so}; pre=${HPK_COMPACT:+compact_}; d=$OUT/pmc_${pre}${wl}${sfx}
         HPK_LIB=loona_amd/$lib timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/fetch -o run -- python3 scripts/dec_time.py $wl 10 > $d.log 2>&1 &&
         HPK_LIB=loona_amd/$lib timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/write -o run -- python3 scripts/dec_time.py $wl 10 >> $d.log 2>&1 &&
-        HPK_LIB=loona_amd/$lib timeout -s KILL 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/pmc_sq_${wl}${sfx} -o run -- python3 scripts/dec_time.py $wl 10 >> $d.log 2>&1 || { echo "pmc $wl $lib failed"; tail $d.log; exit 1; }
+        HPK_LIB=loona_amd/$lib timeout -s KILL 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/pmc_sq_${pre}${wl}${sfx} -o run -- python3 scripts/dec_time.py $wl 10 >> $d.log 2>&1 || { echo "pmc $wl $lib failed"; tail $d.log; exit 1; }
         python3 scripts/pmc_traffic.py $d $n $wl ${KERNEL:-$k} > $d.json &&
-        python3 scripts/pmc_sq.py $OUT/pmc_sq_${wl}${sfx} $n $wl ${KERNEL:-$k} > $OUT/pmc_sq_${wl}${sfx}.json || { echo "pmc summary $wl failed"; exit 1; }
-        cat $d.json $OUT/pmc_sq_${wl}${sfx}.json
+        python3 scripts/pmc_sq.py $OUT/pmc_sq_${pre}${wl}${sfx} $n $wl ${KERNEL:-$k} > $OUT/pmc_sq_${pre}${wl}${sfx}.json || { echo "pmc summary $wl failed"; exit 1; }
+        cat $d.json $OUT/pmc_sq_${pre}${wl}${sfx}.json
       done
     done ;;
   lds)
