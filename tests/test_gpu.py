@@ -896,6 +896,55 @@ def test_large_literals(codec):
     assert (guard == 0xAB).all()
 
 
+@pytest.mark.parametrize("kind", ["decreasing", "past_in_cap"])
+def test_compact_bad_offsets(codec, kind):
+    """The compacted form under bad input offsets (the kernel checks them as it reads them, as in the
+    region form): the offending literals get HPK_BAD_OFFSETS with out_len 0, a synchronous call raises,
+    the literals that did decode match the oracle, and nothing is written past the span out_off[n]
+    reports (guard bytes around the output buffer unchanged)."""
+    from loona_amd import _lib, synth
+    from loona_amd.batch import compact_capacity
+
+    if not codec.compact:
+        pytest.skip("the compacted form only")
+    w = synth.config2(n=20000, seed=8)
+    io = w.enc_off.astype(np.int64).copy()
+    j = 7777
+    if kind == "decreasing":
+        io[j] = io[j + 1] + 3
+    else:
+        io[j + 1 :] += 1 << 20
+    n = w.n
+    guard = 4096
+    need = compact_capacity(w.enc_blob.size, n)
+    big = torch.full((guard + need + guard,), 0xAB, dtype=torch.uint8, device="cuda")
+    out = big[guard:-guard]
+    oo = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    ol = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    dio = to_dev(io.astype(np.uint32).view(np.int32))
+    with pytest.raises(RuntimeError, match="hpk_decode_batch_compact"):
+        codec.decode_compact(to_dev(w.enc_blob), dio, out, oo, ol, st, sync=True)
+    stn, oln = st.cpu().numpy(), ol.cpu().numpy().view(np.uint32)
+    bad = stn == _lib.HPK_BAD_OFFSETS
+    assert bad[j] and (oln[bad] == 0).all()
+    g = big.cpu().numpy()
+    assert (g[:guard] == 0xAB).all() and (g[-guard:] == 0xAB).all()
+    end = int(oo[n].item()) & 0xFFFFFFFF
+    assert (g[guard + end : guard + need] == 0xAB).all(), "bytes written past the reported span"
+    near = np.zeros(n, bool)
+    near[max(0, j - 1) : j + 2] = True  # (literal j - 1 ends at the bad offset: its bytes are not the oracle's)
+    ok = np.nonzero(~bad & ~near)[0]
+    want = oracle_decode_batch(w.enc_blob, w.enc_off)
+    oon = oo.cpu().numpy().view(np.uint32).astype(np.int64)
+    outn = g[guard : guard + need]
+    for i in ok[:: max(1, len(ok) // 2000)]:  # a sample of the literals that decoded
+        assert stn[i] == want[3][i] and oln[i] == want[2][i]
+        s0 = int(want[1][i])
+        assert np.array_equal(outn[oon[i] : oon[i] + oln[i]], want[0][s0 : s0 + oln[i]])
+    codec.check()
+
+
 def test_many_huge_literals(codec):
     """The huge-literal phase (hpk_huge.h) with many huge literals in one workgroup's range: 64 of 8-20
     KiB first (text, random bytes, cut mid-code), then 64k short ones, so the first workgroup lists
