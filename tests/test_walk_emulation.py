@@ -1,14 +1,14 @@
 """The per-lane decode code of the GPU kernels, run on the CPU (no GPU needed).
 
 tests/emu/extract.py lifts the REAL lane-walk functions out of loona_amd/csrc (lit12_body,
-lit12_step with its end detection, lit12_load/status, lo_decode, and hpk_decode_tiny's per-lane body)
-into a host header; tests/emu/shim.h stands in for the handful of HIP builtins they use
-(alignbit, ubfe, perm, clz). tests/emu/emu.cpp replays the kernels' per-lane protocols — the wave
-kernel's body steps then both tails (LUT3 and LUT2), the fill kernel's (LUT2), the small-batch
-kernel lane by lane — on random literals (text, 5-bit-only text that reaches the decoded bound,
-random bytes, EOS runs, bad and too-long padding) at exact-bound regions back to back, below-bound
-regions and bad offsets, against the oracle (oracle/hpk_oracle.c, the checker). What it cannot
-cover — LDS, waves, the fills' staging — is the GPU suite's job (tests/test_gpu.py)."""
+lit12_step with its end detection, lit12_load/status, lo_decode, and the huge-literal phase's
+per-piece functions) into a host header; tests/emu/shim.h stands in for the handful of HIP builtins
+they use (alignbit, ubfe, perm, clz). tests/emu/emu.cpp replays the kernels' per-lane protocols — the
+wave kernel's body steps then both tails (LUT3 and LUT2), the fill kernel's (LUT2), the huge-literal
+phase's passes and fix rounds — on random literals (text, 5-bit-only text that reaches the decoded
+bound, random bytes, EOS runs, bad and too-long padding) in exact-bound regions back to back, against
+the oracle (oracle/hpk_oracle.c, the checker). What it cannot cover — LDS, waves, the fills' staging —
+is the GPU suite's job (tests/test_gpu.py)."""
 
 import os
 import shutil
