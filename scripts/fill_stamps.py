@@ -43,7 +43,7 @@ buf = np.zeros(256 * 16 * 16, np.uint64)
 got = L.hpk_debug_stamps(buf.ctypes.data, buf.size)
 s = buf[:got].reshape(-1, 16).astype(np.int64)
 s = s[s[:, 0] > 0]  # the waves of the launched workgroups
-names = {0: "total", 1: "decode_loop", 2: "steps", 3: "fills", 4: "before_first_fill", 5: "setup_a", 6: "setup_b",
+names = {0: "total", 1: "decode_loop", 2: "steps", 3: "fill_top_barrier_waits", 4: "before_first_fill", 5: "setup_a", 6: "setup_b",
          10: "byte_path", 11: "last_write_back", 12: "setup_b_to_window", 13: "setup_b_to_prefetch",
          14: "setup_b_to_write_back_issue"}
 res = {"literals": n, "kernel_event_us_median": round(float(np.median(times)), 2), "waves": int(s.shape[0])}
