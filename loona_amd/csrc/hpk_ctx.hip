@@ -59,6 +59,9 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     if ((e = hipMalloc(&c->d_lut3, sizeof(t->lut3))) != hipSuccess) return fail("hipMalloc lut3", e);
     if ((e = hipMemcpy(c->d_lut3, t->lut3, sizeof(t->lut3), hipMemcpyHostToDevice)) != hipSuccess)
         return fail("upload lut3", e);
+    if ((e = hipMalloc(&c->d_lut4, sizeof(t->lut4))) != hipSuccess) return fail("hipMalloc lut4", e);
+    if ((e = hipMemcpy(c->d_lut4, t->lut4, sizeof(t->lut4), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail("upload lut4", e);
     if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
     if ((e = hipMalloc(&c->d_t8, sizeof(t->t8))) != hipSuccess) return fail("hipMalloc t8", e);
     if ((e = hipMemcpy(c->d_t8, t->t8, sizeof(t->t8), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload t8", e);
@@ -92,9 +95,11 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
         if (any && !c->long_multi) {  // a second stream: events from here on; the past is drained
             // once, here. (Recording an event on each earlier slot's stream would touch a handle the
             // caller may have destroyed since — a stream bound with hpk_ctx_set_stream, created and
-            // destroyed by the caller: ADVICE r3. A device-wide wait needs no stream handle.)
+            // destroyed by the caller: ADVICE r3.) Launches on a stream the context does not own always
+            // record their slot's event (hpk_long_list_used), so the only slots without one were used on
+            // the context's own stream: waiting for that stream drains them.
             c->long_multi = true;
-            HIP_TRY(hipDeviceSynchronize());
+            HIP_TRY(hipStreamSynchronize(c->own));
             for (int k = 0; k < hpk_ctx::kLongSlots; ++k) c->long_ev_set[k] = false;
         }
         j = 0;
@@ -108,10 +113,7 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
     }
     if (c->long_multi && !c->long_ev[j]) HIP_TRY(hipEventCreateWithFlags(&c->long_ev[j], hipEventDisableTiming));
     if (c->long_list_cap[j] < (size_t)n || !c->long_list[j]) {  // grow: the old list may still be in use
-        if (c->long_ev_set[j])
-            HIP_TRY(hipEventSynchronize(c->long_ev[j]));
-        else if (c->long_list[j])  // single-stream mode on the own stream (foreign streams set events)
-            HIP_TRY(hipStreamSynchronize(c->stream));
+        if (int rc = hpk_slot_drain(c, j)) return rc;
         (void)hipFree(c->long_list[j]);
         c->long_list[j] = nullptr;
         c->long_list_cap[j] = 0;
@@ -121,6 +123,14 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
     }
     *list = c->long_list[j];
     *slot = j;
+    return HPK_E_OK;
+}
+
+int hpk_slot_drain(hpk_ctx* c, int j) {
+    if (c->long_ev_set[j])
+        HIP_TRY(hipEventSynchronize(c->long_ev[j]));
+    else if (c->long_list[j])  // single-stream mode on the own stream (foreign streams set events)
+        HIP_TRY(hipStreamSynchronize(c->stream));
     return HPK_E_OK;
 }
 
@@ -141,6 +151,7 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_lut);
     (void)hipFree(c->d_lut2);
     (void)hipFree(c->d_lut3);
+    (void)hipFree(c->d_lut4);
     (void)hipFree(c->d_lo);
     (void)hipFree(c->d_t8);
     (void)hipFree(c->d_codes);
@@ -149,13 +160,13 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_meta);
     (void)hipFree(c->d_st);
     if (c->h_err) (void)hipHostFree(c->h_err);
-    (void)hipFree(c->d_bound);
-    (void)hipFree(c->d_scan_tmp);
-    (void)hipFree(c->d_cursor);
     if (c->h_pin) (void)hipHostFree(c->h_pin);
     for (int j = 0; j < hpk_ctx::kLongSlots; ++j) {
         if (c->long_ev_set[j]) (void)hipEventSynchronize(c->long_ev[j]);
         if (c->long_list[j]) (void)hipFree(c->long_list[j]);
+        (void)hipFree(c->cp_bound[j]);
+        (void)hipFree(c->cp_tmp[j]);
+        (void)hipFree(c->cp_cursor[j]);
         if (c->long_ev[j]) (void)hipEventDestroy(c->long_ev[j]);
     }
     for (int j = 0; j < hpk_ctx::kMaxChunks; ++j) {
@@ -431,19 +442,27 @@ extern "C" int hpk_decode_batch_compact(hpk_ctx* c, const uint8_t* in_blob, size
         HIP_TRY(hipMemsetAsync(out_off, 0, 4, c->stream));
     } else {
         if (!in_blob || !out_blob) return hpk_set_err_msg("null blob", HPK_E_INVAL);
-        int rc;
-        if ((rc = grow((void**)&c->d_bound, &c->d_bound_cap, ((size_t)n + 1) * 4))) return rc;
-        if (!c->d_cursor) HIP_TRY(hipMalloc(&c->d_cursor, 4));
+        // the stream's slot (two calls on two streams must not share the cursor, the bound
+        // layout or the scan's scratch), its buffers regrown only once its last launch has completed
+        int rc, j;
+        uint32_t* ll = nullptr;
+        if ((rc = hpk_long_list(c, n, &ll, &j))) return rc;
         size_t tmp = 0;
-        if ((rc = hpk_bound_scan(c, in_off, n, c->d_bound, nullptr, &tmp))) return rc;
-        if ((rc = grow(&c->d_scan_tmp, &c->d_scan_tmp_cap, tmp))) return rc;
-        tmp = c->d_scan_tmp_cap;
-        if ((rc = hpk_bound_scan(c, in_off, n, c->d_bound, c->d_scan_tmp, &tmp))) return rc;
-        HIP_TRY(hipMemsetAsync(c->d_cursor, 0, 4, c->stream));
-        const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), c->d_bound, out_len,
+        if ((rc = hpk_bound_scan(c, in_off, n, nullptr, nullptr, &tmp))) return rc;
+        if (c->cp_bound_cap[j] < ((size_t)n + 1) * 4 || c->cp_tmp_cap[j] < tmp || !c->cp_cursor[j]) {
+            if ((rc = hpk_slot_drain(c, j))) return rc;
+            if ((rc = grow((void**)&c->cp_bound[j], &c->cp_bound_cap[j], ((size_t)n + 1) * 4))) return rc;
+            if ((rc = grow(&c->cp_tmp[j], &c->cp_tmp_cap[j], tmp))) return rc;
+            if (!c->cp_cursor[j]) HIP_TRY(hipMalloc(&c->cp_cursor[j], 4));
+        }
+        tmp = c->cp_tmp_cap[j];
+        if ((rc = hpk_bound_scan(c, in_off, n, c->cp_bound[j], c->cp_tmp[j], &tmp))) return rc;
+        HIP_TRY(hipMemsetAsync(c->cp_cursor[j], 0, 4, c->stream));
+        const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), c->cp_bound[j], out_len,
                           status};
-        if ((rc = hpk_launch_decode_compact(c, b, out_off))) return rc;
-        HIP_TRY(hipMemcpyAsync(out_off + n, c->d_cursor, 4, hipMemcpyDeviceToDevice, c->stream));
+        if ((rc = hpk_launch_decode_compact(c, b, out_off, ll, c->cp_cursor[j]))) return rc;
+        HIP_TRY(hipMemcpyAsync(out_off + n, c->cp_cursor[j], 4, hipMemcpyDeviceToDevice, c->stream));
+        if ((rc = hpk_long_list_used(c, j))) return rc;
     }
     if (!(flags & HPK_ASYNC)) {
         HIP_TRY(hipStreamSynchronize(c->stream));

@@ -120,6 +120,7 @@ static void decode_args(hpk_ctx* c, const hpk_batch& b, DecodeArgs& a) {
     a.lut = c->d_lut;
     a.lut2 = c->d_lut2;
     a.lut3 = c->d_lut3;
+    a.lut4 = c->d_lut4;
     a.dbg = nullptr;
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;
@@ -140,22 +141,19 @@ static uint32_t decode_blocks(hpk_ctx* c, const hpk_batch& b) {
     return (uint32_t)blocks;
 }
 
-int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off) {
+int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor) {
     DecodeArgs a;
     decode_args(c, b, a);
     a.lit_out = co_off;
     a.co_off = co_off;
-    a.cursor = c->d_cursor;
-    uint32_t* ll = nullptr;
-    int lslot = 0;
-    if (int rc = hpk_long_list(c, b.n, &ll, &lslot)) return rc;
-    a.long_list = ll;
+    a.cursor = cursor;
+    a.long_list = long_list;
     a.long_min = HPK_LONG_MIN;
     a.long_big = HPK_LONG_BIG;
     hipLaunchKernelGGL((hpk_decode12<0, kWaves, kW, kO, kQ, kRefillN, true>), dim3(decode_blocks(c, b)),
                        dim3(Geo::kBlock), 0, c->stream, a);
     HIP_TRY(hipGetLastError());
-    return hpk_long_list_used(c, lslot);
+    return HPK_E_OK;
 }
 
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {

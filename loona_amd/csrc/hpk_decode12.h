@@ -120,6 +120,7 @@ struct Lit12 {
     bool more;            // (kMore steps) the walk may go on: the last step used both entries whole, or
                           // decoded a long code; false once a step has proved that no code fits
     bool act;             // holds a fast-path literal not yet finalised
+    uint32_t pe1, pe2;    // (lit_or_body) the last body step's two entries, stored by the next step
 };
 
 // (Re)load the pair and the next dword at X.
@@ -310,6 +311,125 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
 __device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
     if (L.st != HPK_OK) return L.st;
     return residual_status(L.Eb - L.X, __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X));
+}
+
+// ------------------------------------------------------------------------------------------
+// Dword output (decode v31, the wave kernel's fills). The literal is decoded into a ZEROED LDS image
+// by atomic ORs of whole dwords: a step's decoded bytes (up to four, zero above them) are shifted to
+// the output position's byte lane and OR-ed into the dword there and the next one (ds_or_b32, no
+// return). Two LDS stores per step replace four byte stores, and the dwords two literals share at
+// their edges need no order between the lanes that write them: an OR of zero bytes changes nothing.
+// L.o holds the output position in BITS (8 x the LDS byte address): the LUT4 entries' top bytes
+// advance it, and its low five bits are the shift that places a step's bytes. Semantics are
+// lit12_body's / lit12_step's (huffman.rs:95-161); only the stores differ.
+#ifndef HPK_SCHED_FENCE
+#define HPK_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+__device__ __forceinline__ void or_dword(uint32_t* __restrict__ img32, uint32_t d, uint32_t v) {
+    __hip_atomic_fetch_or(&img32[d], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void or_out(uint32_t* __restrict__ img32, uint32_t o8, uint32_t v) {
+    const uint64_t t = (uint64_t)v << (o8 & 24u);
+    or_dword(img32, o8 >> 5, (uint32_t)t);
+    or_dword(img32, (o8 >> 5) + 1u, (uint32_t)(t >> 32));
+}
+
+// The leading-ones branch of both steps: a 13..30-bit code or EOS at X with > 12 bits left.
+__device__ __forceinline__ void lit_or_long(Lit12& L, const uint32_t* __restrict__ win32, const uint16_t* __restrict__ lo,
+                                            uint32_t* __restrict__ img32) {
+    const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    uint32_t sy, len;
+    bool eos;
+    lo_decode(wp, lo, sy, len, eos);
+    const uint32_t r = L.Eb - L.X;
+    if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+        L.st = HPK_PADDING_TOO_LARGE;
+        L.Eb = L.X;
+        L.more = false;
+    } else if (eos) {  // huffman.rs:112-116
+        L.st = HPK_EOS_IN_STRING;
+        L.Eb = L.X;
+        L.more = false;
+    } else {
+        or_dword(img32, L.o >> 5, sy << (L.o & 24u));  // (one byte: never crosses a dword)
+        L.o += 8u;
+        L.X += len;
+        lit12_load(L, win32);
+    }
+}
+
+// The bytes of a body step's two entries (pe1, pe2), OR-ed at L.o, which then moves past them.
+__device__ __forceinline__ void lit_or_pend(Lit12& L, uint32_t* __restrict__ img32) {
+    or_out(img32, L.o, (L.pe1 & 0xFFFFu) | ((L.pe2 & 0xFFFFu) << HPK_L4_C8(L.pe1)));
+    L.o += HPK_L4_C8(L.pe1) + HPK_L4_C8(L.pe2);
+    L.pe1 = L.pe2 = 0u;
+}
+
+// Body step: lit12_body's two unchecked lookups (>= kBodyMin bits left), bytes OR-ed as a dword pair.
+// Software-pipelined: a step's entries are kept (pe1, pe2) and stored by the NEXT step while its first
+// lookup is in flight, so the walk's dependency chain (bit position -> window -> lookup -> lookup ->
+// bit position) carries no store work; lit_or_pend stores the last step's at the body's end.
+__device__ __forceinline__ void lit_or_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                            const uint16_t* __restrict__ lo, uint32_t* __restrict__ img32, bool& body) {
+    const uint32_t d3 = win32[(L.X >> 5) + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+    HPK_SCHED_FENCE();
+    lit_or_pend(L, img32);  // the previous step's bytes, under this step's first lookup
+    HPK_SCHED_FENCE();
+    const uint32_t e2 = lut[(w << ((e1 >> 16) & 31u)) >> (32 - HPK_LUT_BITS)];
+    const uint32_t u2 = HPK_L4_HELD(e2);
+    const uint32_t xn = L.X + HPK_L4_HELD(e1) + u2;
+    const bool cross = (xn ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xn;
+    L.pe1 = e1;
+    L.pe2 = e2;
+    if (u2 == 0u) {  // e2 holds no code (nor e1, if it held none): its bytes first, then the long code's
+        lit_or_pend(L, img32);
+        lit_or_long(L, win32, lo, img32);
+    }
+    body = L.Eb - L.X >= kBodyMin;
+}
+
+// Checked step (the tails): lit12_step<.., kMore>'s fit tests, from LUT4's fields.
+__device__ __forceinline__ void lit_or_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                            const uint16_t* __restrict__ lo, uint32_t* __restrict__ img32) {
+    const uint32_t d3 = win32[(L.X >> 5) + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t rem = L.Eb - L.X;
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+    const uint32_t c1 = HPK_L4_C8(e1), h1 = HPK_L4_HELD(e1), l1 = HPK_L4_LEN0(e1);
+    const bool a1 = (c1 != 0u) & (l1 <= rem);
+    const bool a2 = (c1 == 16u) & (h1 <= rem);
+    const uint32_t u1 = a2 ? h1 : (a1 ? l1 : 0u);
+    // a code longer than 12 bits (or EOS) starts here and may still fit (with more than 12 bits left,
+    // any code the entry holds fits: no first code <=> the entry has none)
+    bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
+    const bool cont = a1 & (a2 | (c1 != 16u));  // the first entry was consumed whole
+    const uint32_t rem2 = rem - u1;
+    const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
+    const uint32_t c2 = HPK_L4_C8(e2), h2 = HPK_L4_HELD(e2), l2 = HPK_L4_LEN0(e2);
+    const bool b1 = cont & (c2 != 0u) & (l2 <= rem2);
+    const bool b2 = cont & (c2 == 16u) & (h2 <= rem2);
+    park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
+    // both entries used whole: more codes may follow (otherwise the walk has ended, huffman.rs:100-123)
+    const bool more2 = b1 & (b2 | (c2 != 16u));
+    const uint32_t g1 = 8u * ((uint32_t)a1 + (uint32_t)a2), g2 = 8u * ((uint32_t)b1 + (uint32_t)b2);
+    const uint32_t v = __builtin_amdgcn_ubfe(e1, 0, g1) | (__builtin_amdgcn_ubfe(e2, 0, g2) << g1);
+    or_out(img32, L.o, v);
+    L.o += g1 + g2;
+    const uint32_t xn = L.X + u1 + (b2 ? h2 : (b1 ? l2 : 0u));
+    const bool cross = (xn ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xn;
+    L.prog = a1 | park;
+    L.more = park | more2;
+    if (park) lit_or_long(L, win32, lo, img32);
 }
 
 }  // namespace hpkdec

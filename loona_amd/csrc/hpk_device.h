@@ -18,6 +18,7 @@ struct hpk_ctx {
     uint32_t* d_lut = nullptr;
     uint32_t* d_lut2 = nullptr;
     uint32_t* d_lut3 = nullptr;
+    uint32_t* d_lut4 = nullptr;
     uint16_t* d_lo = nullptr;
     uint8_t* d_t8 = nullptr;
     uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length
@@ -56,12 +57,13 @@ struct hpk_ctx {
     int long_next = 0;
     bool long_multi = false;  // more than one stream has used the context: slots carry events
     // the compacted mode (hpk_decode_batch_compact): the fills' bound layout, the scan's scratch and the
-    // output cursor, grow-only
-    uint32_t* d_bound = nullptr;
-    size_t d_bound_cap = 0;
-    void* d_scan_tmp = nullptr;
-    size_t d_scan_tmp_cap = 0;
-    uint32_t* d_cursor = nullptr;
+    // output cursor, per slot like the long-literal list (two calls on two streams never share them),
+    // grow-only
+    uint32_t* cp_bound[kLongSlots] = {};
+    size_t cp_bound_cap[kLongSlots] = {};
+    void* cp_tmp[kLongSlots] = {};
+    size_t cp_tmp_cap[kLongSlots] = {};
+    uint32_t* cp_cursor[kLongSlots] = {};
 };
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on
@@ -69,6 +71,8 @@ struct hpk_ctx {
 int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot);
 // Records the slot's event on the context's stream after the launch that reads the list.
 int hpk_long_list_used(hpk_ctx* c, int slot);
+// Waits until the slot's last launch has completed (before its buffers are freed or regrown).
+int hpk_slot_drain(hpk_ctx* c, int slot);
 
 // One batch call as the launchers see it: capacities clamped to HPK_MAX_OFFSET (offsets above
 // them are bad whatever the buffer size).
@@ -95,8 +99,9 @@ int hpk_set_err_msg(const char* what, int code);
 
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b);
 // The compacted mode: b.out_off is the bound layout made by hpk_bound_scan, co_off the caller's output
-// offsets, c->d_cursor the (zeroed) output cursor.
-int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off);
+// offsets, cursor the (zeroed) output cursor, long_list the slot's long-literal list (the caller took the
+// slot with hpk_long_list and records it used after its last operation on the stream).
+int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor);
 // out[i] = sum over j < i of the 4-rounded decoded bound of literal j (n + 1 entries), on the ctx
 // stream; tmp == nullptr: *tmp_bytes = the scratch it needs.
 int hpk_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out, void* tmp, size_t* tmp_bytes);

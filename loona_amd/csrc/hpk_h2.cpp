@@ -12,6 +12,7 @@
 // batch. A block whose CONTINUATION frames have not all arrived stays with its connection until a
 // later call completes it; a connection error stops that connection, as the reference's connection
 // task ends with GOAWAY.
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>

@@ -44,6 +44,10 @@
 #ifndef HPK_LUT3
 #define HPK_LUT3 1  // v28: the wave kernel's lookups in the LUT3 layout (byte-wide "bits held")
 #endif
+#ifndef HPK_WAVE_OR
+#define HPK_WAVE_OR 0  // 1: fills decode into a zeroed image by dword ORs (lit_or_body / lit_or_step, LUT4):
+                       // measured 882-899 us against 855-870 (round 5, profiles/r05/ab_or_output_rejected.jsonl)
+#endif
 
 namespace hpkdec {
 
@@ -103,9 +107,12 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
-    constexpr int kTab = HPK_LUT3 && HPK_BODY ? 3 : 2;
+    constexpr int kTab = HPK_LUT3 && HPK_BODY ? 3 : 2;  // (the long and huge phases' layout)
+    // v31: the fills' steps OR whole dwords into a zeroed image (LUT4); the long and huge phases get
+    // the LUT3 / LUT2 layout back after the fills
+    constexpr bool kOr = HPK_WAVE_OR && HPK_BODY && kMode != 1 && kMode != 2 && !(kMode >= 6 && kMode <= 10);
     for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
-        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kOr ? a.lut4 : kTab == 3 ? a.lut3 : a.lut2)[t];
     if (tid < 16) s_ctr[tid] = 0;
     if (kMode == 3)
         for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
@@ -188,6 +195,11 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         const uint32_t* const wl32 = reinterpret_cast<const uint32_t*>(smem);
         uint8_t* const ol8 = smem;
         const uint32_t dmy = obase + (uint32_t)G::kImg + lane * 4u;
+        uint32_t* const img32 = reinterpret_cast<uint32_t*>(smem);
+        if (kOr) {  // the image starts zeroed (then the write-back zeroes what it has read out)
+            uint4* l16 = reinterpret_cast<uint4*>(s_img);
+            for (uint32_t i = lane; i < (uint32_t)G::kImg / 16u; i += 64u) l16[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
         // The workgroup's range is handed out in chunks, in order, to whichever wave asks next (an LDS
         // cursor): a static split left the waves the SIMDs' arbitration favours idle at the end while
         // the others finished (11 % of a wave's time). Chunks shrink as the range drains (guided
@@ -204,7 +216,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             }
             uint32_t c = 0;
             if (lane == 0) {
-                const uint32_t seen = *reinterpret_cast<volatile uint32_t*>(&s_ctr[7]);
+                const uint32_t seen = *(volatile HPK_LDS_AS uint32_t*)(&s_ctr[7]);
                 const uint32_t left = BB - BA > seen ? BB - BA - seen : 0u;
                 const uint32_t want = max(kChunk, left / 32u);
                 c = atomicAdd(&s_ctr[7], want);
@@ -259,19 +271,23 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         auto flush = [&]() {  // the previous fill's image span and results to global memory
             const uint32_t ob = pG0 & ~15u;
             const uint32_t c0 = ob >> 4, c1 = (pG1 + 15u) >> 4;
-            const uint4* l16 = reinterpret_cast<const uint4*>(s_img) + (opaque(lane) - lane);
+            uint4* l16 = reinterpret_cast<uint4*>(s_img) + (opaque(lane) - lane);
             uint4* g16 = reinterpret_cast<uint4*>(a.out_base);
             if (kMode != 2) {
-#pragma unroll
-                for (int r = 0; r < F; ++r) {
-                    const uint32_t ci = c0 + lane + 64u * r;
-                    if (ci < c1 && (ci << 4) >= pG0 && (ci << 4) + 16u <= pG1) g16[ci] = l16[ci - c0];
-                }
-                if (lane < 32) {  // the partial chunks at the two ends, one byte per lane
+                if (lane < 32) {  // the partial chunks at the two ends, one byte per lane (read before the
+                                  // chunks are zeroed below)
                     const uint32_t g = lane < 16 ? c0 << 4 : (c1 - 1u) << 4;
                     const bool partial = !(g >= pG0 && g + 16u <= pG1) && (lane < 16 || c1 - 1u != c0);
                     const uint32_t x = g + (lane & 15u);
                     if (partial && x >= pG0 && x < pG1) a.out_base[x] = s_img[x - ob];
+                }
+#pragma unroll
+                for (int r = 0; r < F; ++r) {
+                    const uint32_t ci = c0 + lane + 64u * r;
+                    if (ci < c1) {
+                        if ((ci << 4) >= pG0 && (ci << 4) + 16u <= pG1) g16[ci] = l16[ci - c0];
+                        if (kOr) l16[ci - c0] = make_uint4(0u, 0u, 0u, 0u);
+                    }
                 }
             }
             if (ri0 != 0xFFFFFFFFu) {
@@ -368,10 +384,24 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     gout_n = a.out_off[cur_n] + a.out_mis;
                 }
             }
-            // 2. the previous fill's write-back (its image is read out before this fill's queue lands there)
+            // 2. the window, big-endian dwords: bit P of the stream is bit 31 - P % 32 of dword P / 32
+            // (staged before the write-back's stores are issued: its loads' vmcnt wait then covers no
+            // store of this fill)
+            {
+                uint4* l16 = reinterpret_cast<uint4*>(s_win) + (opaque(lane) - lane);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint4 c = ch[r];
+                    if (lane + 64u * r < (uint32_t)kWinB / 16u)
+                        l16[lane + 64u * r] = make_uint4(__builtin_bswap32(c.x), __builtin_bswap32(c.y),
+                                                         __builtin_bswap32(c.z), __builtin_bswap32(c.w));
+                }
+            }
+            stamp(4);
+            // 3. the previous fill's write-back (its image is read out before this fill's queue lands there)
             if (pk) flush();
             stamp(2);
-            // 3. queue, longest first (kRank 0: a counting sort over 32 length classes of 2 bytes, 996-1015
+            // 4. queue, longest first (kRank 0: a counting sort over 32 length classes of 2 bytes, 996-1015
             // us on config 5 against 1121-1175 us for the ballot ranks, r3h/r3j), long literals listed
             // for the long-literal phase instead
             bool qd[2];
@@ -420,26 +450,27 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             if (qd[0]) q[rank0] = make_uint2(ex[0], ey[0]);
             if (qd[1]) q[rank1] = make_uint2(ex[1], ey[1]);
             stamp(3);
-            // 4. the window, big-endian dwords: bit P of the stream is bit 31 - P % 32 of dword P / 32
-            {
-                uint4* l16 = reinterpret_cast<uint4*>(s_win) + (opaque(lane) - lane);
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint4 c = ch[r];
-                    if (lane + 64u * r < (uint32_t)kWinB / 16u)
-                        l16[lane + 64u * r] = make_uint4(__builtin_bswap32(c.x), __builtin_bswap32(c.y),
-                                                         __builtin_bswap32(c.z), __builtin_bswap32(c.w));
-                }
-            }
-            stamp(4);
             // 5. the snake's two queue entries per lane (read before the image is decoded over), and
             // the workgroup's stop flag for the next fill
             const uint32_t t1 = lane, t2 = 127u - lane;
             const uint2 e1 = kq ? q[min(t1, kq - 1u)] : make_uint2(0u, 0u);
             const uint2 e2 = kq ? q[min(t2, kq - 1u)] : make_uint2(0u, 0u);
-            stop = *reinterpret_cast<volatile uint32_t*>(&s_ctr[0]);
-            // 6. the next fill's offsets and window, in flight while this one decodes
-            if (cur_n < ce_n) prefetch(cur_n, ce_n, gin_n & ~15u);
+            // (through an LDS-qualified pointer: a volatile read through a generic one is a flat load,
+            // and its vmcnt(0) wait made every fill wait for its own write-back's stores)
+            stop = *(volatile HPK_LDS_AS uint32_t*)(&s_ctr[0]);
+            if (kOr) {  // the counting sort's classes and the queue (image bytes [0, 1280)) zeroed again
+                uint4* l16 = reinterpret_cast<uint4*>(s_img) + (opaque(lane) - lane);
+                l16[lane] = make_uint4(0u, 0u, 0u, 0u);
+                if (lane < 16) l16[64u + lane] = make_uint4(0u, 0u, 0u, 0u);
+            }
+            // 6. the next fill's offsets and window, in flight while this one decodes. Issued
+            // unconditionally (past the last chunk: this fill's again, never used): under a branch the
+            // registers' old and new values met in copies, and a copy waits for its load (vmcnt(0)
+            // right after the loads: every fill waited for the next fill's offsets)
+            {
+                const bool more = cur_n < ce_n;
+                prefetch(more ? cur_n : cur, more ? ce_n : cur + k, (more ? gin_n : gin) & ~15u);
+            }
             // 7. lane walks: slots t1 then t2
             Lit12 L, N;
             auto load = [&](Lit12& T, const uint2 e, uint32_t tt) {
@@ -449,10 +480,11 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const uint32_t o = (e.y >> 12) & 0x1FFFFu;
                 T.X = wbits + (e.x & 0xFFFFu) * 8u + 31u;
                 T.Eb = T.X + (T.act ? nb * 8u : 0u);
-                T.o = obase + o;
+                T.o = kOr ? (obase + o) * 8u : obase + o;  // (v31: in bits)
                 T.o0 = obase + o;
                 T.st = HPK_OK;
                 T.prog = false;
+                T.pe1 = T.pe2 = 0u;
                 lit12_load(T, wl32);
             };
             load(L, e1, t1);
@@ -474,7 +506,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     dg_add(9, 1u);
 #pragma unroll
                     for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
-                        if (body)
+                        if (body && kOr)
+                            lit_or_body(L, wl32, s_lut, s_lo, img32, body);
+                        else if (body)
                             lit12_body<kStore, kTab, (kMode >= 8 && kMode <= 10) ? kMode - 7 : 0>(L, wl32, s_lut, s_lo,
                                                                                                    ol8, body);
                         if (kMode == 6) {
@@ -491,6 +525,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                         const bool sw = !body & onA;
                         if (sw) {  // the first literal's body is done: it waits, the second one starts (its
                                    // state made from the queue entry here, not carried through the loop)
+                            if (kOr) lit_or_pend(L, img32);
                             aX = L.X;
                             aO = L.o;
                             aSt = L.st;
@@ -505,29 +540,35 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 // tails: both literals of the lane at once, t1's from where its body stopped (restored
                 // into L), t2's (in N) from where its body stopped; a step that proves the walk has
                 // ended clears `more`, so no step is spent finding out (usually one step per tail)
+                if (kOr) lit_or_pend(L, img32);
                 N = L;
                 L.X = aX;
                 L.o = aO;
                 L.st = aSt;
                 L.act = aAct;
                 L.Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (aAct ? (e1.x >> 16) * 8u : 0u);
-                L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);
+                L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);  // (bytes; L.o in bits when kOr)
                 L.idx = e1.y & 0xFFFu;
                 if (aSt != HPK_OK) L.Eb = L.X;  // ended in its body (EOS / padding): no tail
                 lit12_load(L, wl32);
                 L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
                 N.more = N.Eb - N.X >= 5u;
                 while (__any(L.more | N.more)) {
-                    if (L.more) lit12_step<kStore, true, kTab, true>(L, wl32, s_lut, s_lo, ol8, dmy);
-                    if (N.more) lit12_step<kStore, true, kTab, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                    if (kOr) {
+                        if (L.more) lit_or_step(L, wl32, s_lut, s_lo, img32);
+                        if (N.more) lit_or_step(N, wl32, s_lut, s_lo, img32);
+                    } else {
+                        if (L.more) lit12_step<kStore, true, kTab, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                        if (N.more) lit12_step<kStore, true, kTab, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                    }
                 }
                 // results in the v26 form: the first slot's end state saved, the second in L
                 sX = L.X;
-                sO = L.o;
+                sO = kOr ? L.o >> 3 : L.o;
                 sSt = L.st;
                 s1 = L.act;
                 L = N;
-                Lend = L.o;
+                Lend = kOr ? L.o >> 3 : L.o;
             } else if (kMode != 1) {
                 for (;;) {
                     dg_add(9, 1u);
@@ -618,9 +659,13 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     }
     // ---- the literals left to the long-literal phase ----
     __syncthreads();  // every wave's fills, list entries and stores are out
-    const uint32_t c1 = s_ctr[1], c2 = s_ctr[2];
-    huge_phase<G::kBlock, kTab>(a, s_huge, min(s_ctr[8], kHugeMax), reinterpret_cast<uint32_t*>(smem + G::kWaveOff),
-                                s_lut, s_lo);
+    const uint32_t c1 = s_ctr[1], c2 = s_ctr[2], nh = min(s_ctr[8], kHugeMax);
+    if (kOr && c1 + c2 + nh != 0u) {  // (block-uniform) the phases' table layout
+        for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
+            reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
+        __syncthreads();
+    }
+    huge_phase<G::kBlock, kTab>(a, s_huge, nh, reinterpret_cast<uint32_t*>(smem + G::kWaveOff), s_lut, s_lo);
     if (c1 + c2) {
         static_assert(G::kWaveOff % 16 == 0, "long-phase rings");
         uint8_t* const area = smem + G::kWaveOff;

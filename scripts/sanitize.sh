@@ -1,0 +1,41 @@
+#!/bin/bash
+# Sanitizer builds of the host code, CPU only (no GPU sanitizer exists on this pool):
+#   asan  hpk_cpu.cpp, hpk_hpack.cpp, hpk_h2.cpp and the oracle with -fsanitize=address,undefined
+#   tsan  the same host sources with -fsanitize=thread (the 16-thread pool of the block decoder, the
+#         threaded CPU batch paths, the fork handling)
+# Each links the unsanitized device objects (hpk_ctx/decode/encode, built by the Makefile) into
+# loona_amd/libhpk_<kind>.so and runs the CPU suite against it (HPK_LIB / HPK_ORACLE_LIB select the
+# libraries, LD_PRELOAD puts the sanitizer runtime ahead of the uninstrumented python). A report
+# fails the run (halt_on_error / exitcode). Usage: scripts/sanitize.sh [asan|tsan|all] [pytest args]
+set -eo pipefail
+cd "$(dirname "$0")/.."
+KIND=${1:-all}; shift || true
+CS=loona_amd/csrc
+make -s -C $CS hpk_ctx.o hpk_decode.o hpk_encode.o
+DEV="$CS/hpk_ctx.o $CS/hpk_decode.o $CS/hpk_encode.o"
+HIPLIB="-L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64"
+build() {  # kind flags
+  local k=$1 f=$2 T=/tmp/hpk_san_$1; mkdir -p $T
+  for s in hpk_cpu hpk_hpack hpk_h2; do
+    g++ -std=c++17 -O1 -g -fPIC -fno-omit-frame-pointer $f -I/opt/rocm/include -c $CS/$s.cpp -o $T/$s.o
+  done
+  g++ -shared -fPIC $f -o loona_amd/libhpk_$k.so $T/hpk_cpu.o $T/hpk_hpack.o $T/hpk_h2.o $DEV $HIPLIB -lpthread
+  echo "built loona_amd/libhpk_$k.so"
+}
+run() {  # kind runtime options-var
+  local k=$1 rt=$2
+  echo "== pytest -m 'not gpu' under $k"
+  env LD_PRELOAD="$(gcc -print-file-name=$rt)" HPK_LIB=$PWD/loona_amd/libhpk_$k.so "${@:3}" \
+    python -m pytest tests -m "not gpu" -x -q -p no:cacheprovider $PYTEST_ARGS
+}
+if [ "$KIND" = asan ] || [ "$KIND" = all ]; then
+  build asan "-fsanitize=address,undefined -fno-sanitize-recover=undefined"
+  make -s -C oracle asan
+  run asan libasan.so HPK_ORACLE_LIB=$PWD/oracle/liboracle_asan.so \
+    ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
+fi
+if [ "$KIND" = tsan ] || [ "$KIND" = all ]; then
+  build tsan "-fsanitize=thread"
+  run tsan libtsan.so TSAN_OPTIONS=halt_on_error=1:exitcode=66:report_signal_unsafe=0
+fi
+echo "sanitizers: clean"

@@ -25,3 +25,6 @@ struct uint4 { uint32_t x, y, z, w; };
 struct emu_dim3 { uint32_t x = 0, y = 0, z = 0; };
 extern emu_dim3 threadIdx, blockIdx;
 static inline uint32_t hpk_bswap32(uint32_t x) { return __builtin_bswap32(x); }
+#define __HIP_MEMORY_SCOPE_WORKGROUP 0
+static inline uint32_t __hip_atomic_fetch_or(uint32_t* p, uint32_t v, int, int) { const uint32_t o = *p; *p = o | v; return o; }
+#define HPK_SCHED_FENCE() do { } while (0)

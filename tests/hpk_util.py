@@ -20,7 +20,8 @@ _oracle = None
 def oracle():
     global _oracle
     if _oracle is None:
-        L = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        # HPK_ORACLE_LIB: the sanitizer build of the same oracle (scripts/sanitize.sh)
+        L = ctypes.CDLL(os.environ.get("HPK_ORACLE_LIB", os.path.join(REPO, "oracle", "liboracle.so")))
         L.oracle_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_decode.restype = ctypes.c_int

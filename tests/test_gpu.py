@@ -1052,3 +1052,28 @@ def test_exact_bound_regions_short_literals(codec):
         got, guard = _decode_regions(codec, blob, off, bound, shift=shift)
         compare_batches(got, ref, f"exact-bound short literals at +{shift}")
         assert (guard == 0xAB).all()
+
+
+def test_compact_two_streams_overlap(codec):
+    """two HPK_ASYNC compacted calls on two streams at once. Each call takes its stream's
+    slot of the context (cursor, bound layout, scan scratch, long-literal list), so the second call's
+    cursor reset and scan cannot reach the first call's kernel. A large batch on stream 1 is issued
+    first, then a different small batch on stream 2; both are checked byte for byte against their
+    generated strings, and the layouts must be disjoint and inside each call's capacity."""
+    from loona_amd import HuffmanCodec, synth
+
+    big = synth.device_config2(codec, n=2_000_000, seed=101)
+    small = synth.device_config2(codec, n=20_000, seed=202)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with HuffmanCodec(0, stream="own") as c:
+        for rep in range(3):
+            c.set_stream(s1)
+            r1 = c.decode_compact(big.enc_blob, big.enc_off, sync=False)
+            c.set_stream(s2)
+            r2 = c.decode_compact(small.enc_blob, small.enc_off, sync=False)
+            torch.cuda.synchronize()
+            c.check()
+            for w, (out, oo, ol, st) in ((big, r1), (small, r2)):
+                _check_compact(out, oo, ol, w.n)
+                synth.check_decoded(w, out, oo, ol, st)
