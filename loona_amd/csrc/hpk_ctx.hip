@@ -460,8 +460,11 @@ extern "C" int hpk_decode_batch_compact(hpk_ctx* c, const uint8_t* in_blob, size
         HIP_TRY(hipMemsetAsync(c->cp_cursor[j], 0, 4, c->stream));
         const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), c->cp_bound[j], out_len,
                           status};
-        if ((rc = hpk_launch_decode_compact(c, b, out_off, ll, c->cp_cursor[j]))) return rc;
-        HIP_TRY(hipMemcpyAsync(out_off + n, c->cp_cursor[j], 4, hipMemcpyDeviceToDevice, c->stream));
+        int wave = 0;
+        if ((rc = hpk_launch_decode_compact(c, b, out_off, ll, c->cp_cursor[j], &wave))) return rc;
+        // the span written: the cursor (workgroup-fill kernel), or the bound layout's end (wave-fill kernel)
+        HIP_TRY(hipMemcpyAsync(out_off + n, wave ? c->cp_bound[j] + n : c->cp_cursor[j], 4, hipMemcpyDeviceToDevice,
+                               c->stream));
         if ((rc = hpk_long_list_used(c, j))) return rc;
     }
     if (!(flags & HPK_ASYNC)) {

@@ -141,7 +141,11 @@ static uint32_t decode_blocks(hpk_ctx* c, const hpk_batch& b) {
     return (uint32_t)blocks;
 }
 
-int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor) {
+// The compacted form: the wave-fill kernel's (each workgroup packs into its range's bound span, no device
+// cursor: *wave = 1, out_off[n] is then the bound layout's end) for the batches the region form runs it
+// on, else the workgroup-fill kernel's (fills packed from the device cursor, *wave = 0)
+int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor,
+                              int* wave) {
     DecodeArgs a;
     decode_args(c, b, a);
     a.lit_out = co_off;
@@ -150,8 +154,15 @@ int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, 
     a.long_list = long_list;
     a.long_min = HPK_LONG_MIN;
     a.long_big = HPK_LONG_BIG;
-    hipLaunchKernelGGL((hpk_decode12<0, kWaves, kW, kO, kQ, kRefillN, true>), dim3(decode_blocks(c, b)),
-                       dim3(Geo::kBlock), 0, c->stream, a);
+    *wave = c->decode_kernel == HPK_DECODE_WAVE || (c->decode_kernel == HPK_DECODE_AUTO && b.n >= HPK_WAVE_MIN);
+    if (*wave) {
+        a.cursor = nullptr;  // (the huge phase takes a listed literal's region from co_off)
+        hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, HPK_WAVE_CHUNK, HPK_WAVE_GUIDED, HPK_WAVE_RANK, true>),
+                           dim3(decode_blocks(c, b)), dim3(Geo::kBlock), 0, c->stream, a);
+    } else {
+        hipLaunchKernelGGL((hpk_decode12<0, kWaves, kW, kO, kQ, kRefillN, true>), dim3(decode_blocks(c, b)),
+                           dim3(Geo::kBlock), 0, c->stream, a);
+    }
     HIP_TRY(hipGetLastError());
     return HPK_E_OK;
 }

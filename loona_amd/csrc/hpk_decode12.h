@@ -74,6 +74,12 @@ __device__ __forceinline__ uint32_t win_at(const uint32_t* __restrict__ win32, u
 template <int kTab = 2>  // the table layout: 2 = LUT2, 3 = LUT3 (hpk_code.h)
 __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
     // a length field the entry does not hold is 15, past any clamped rem (and t1 >= l1: ok2 => ok1)
+    if (kTab == 4) {  // LUT4: 8 x codes held in [31:24], len0 - 5 in [23:21], bits held in [20:16]
+        const uint32_t c8 = HPK_L4_C8(e), t1 = HPK_L4_HELD(e), l1 = HPK_L4_LEN0(e);
+        ok1 = (c8 != 0u) & (l1 <= rem);
+        ok2 = (c8 == 16u) & (t1 <= rem);
+        return ok2 ? t1 : (ok1 ? l1 : 0u);
+    }
     const uint32_t rc = min(rem, HPK_LUT2_CLAMP);
     if (kTab == 3) {
         const uint32_t l1 = HPK_L3_LEN0(e), t1 = HPK_L3_HELD(e);
@@ -88,7 +94,12 @@ __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, b
 }
 template <int kTab>
 __device__ __forceinline__ bool lut_nottwo(uint32_t e) {
-    return kTab == 3 ? e >= HPK_L3_NOTTWO : e >= HPK_LUT2_NOTTWO;
+    return kTab == 4 ? HPK_L4_C8(e) != 16u : kTab == 3 ? e >= HPK_L3_NOTTWO : e >= HPK_LUT2_NOTTWO;
+}
+// An entry's second symbol byte, in place for a byte store (LUT2 / LUT3: [23:16], LUT4: [15:8])
+template <int kTab>
+__device__ __forceinline__ uint32_t lut_sym1(uint32_t e) {
+    return kTab == 4 ? e >> 8 : e >> 16;
 }
 
 // The decoded bytes of an entry, packed little-endian and zero above the g = ok1 + ok2 of them.
@@ -121,6 +132,7 @@ struct Lit12 {
                           // decoded a long code; false once a step has proved that no code fits
     bool act;             // holds a fast-path literal not yet finalised
     uint32_t pe1, pe2;    // (lit_or_body) the last body step's two entries, stored by the next step
+    uint32_t acc;         // (lit_acc_body) the pending dword's bytes below the output position
 };
 
 // (Re)load the pair and the next dword at X.
@@ -157,12 +169,12 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     if (kStore == kPred) {
         out8[a1 ? L.o : dmy] = (uint8_t)e1;
         if (kP1)
-            (out8 + 1)[a2 ? L.o : dmy - 1u] = (uint8_t)(e1 >> 16);
+            (out8 + 1)[a2 ? L.o : dmy - 1u] = (uint8_t)lut_sym1<kTab>(e1);
         else
-            out8[a2 ? L.o + 1 : dmy] = (uint8_t)(e1 >> 16);
+            out8[a2 ? L.o + 1 : dmy] = (uint8_t)lut_sym1<kTab>(e1);
     } else {
         if (a1) put8(out8, L.o, e1, L.oend, kStore);
-        if (a2) put8(out8, L.o + 1, e1 >> 16, L.oend, kStore);
+        if (a2) put8(out8, L.o + 1, lut_sym1<kTab>(e1), L.oend, kStore);
     }
     L.o += (uint32_t)a1 + (uint32_t)a2;
     {
@@ -182,12 +194,12 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
         if (kStore == kPred) {
             out8[b1 ? L.o : dmy] = (uint8_t)e2;
             if (kP1)
-                (out8 + 1)[b2 ? L.o : dmy - 1u] = (uint8_t)(e2 >> 16);
+                (out8 + 1)[b2 ? L.o : dmy - 1u] = (uint8_t)lut_sym1<kTab>(e2);
             else
-                out8[b2 ? L.o + 1 : dmy] = (uint8_t)(e2 >> 16);
+                out8[b2 ? L.o + 1 : dmy] = (uint8_t)lut_sym1<kTab>(e2);
         } else {
             if (b1) put8(out8, L.o, e2, L.oend, kStore);
-            if (b2) put8(out8, L.o + 1, e2 >> 16, L.oend, kStore);
+            if (b2) put8(out8, L.o + 1, lut_sym1<kTab>(e2), L.oend, kStore);
         }
         L.o += (uint32_t)b1 + (uint32_t)b2;
         use += cont ? u2 : 0u;
@@ -255,29 +267,29 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
     if (kDup == 2) asm volatile("" ::"v"(((const volatile HPK_LDS_AS uint32_t*)win32)[(L.X >> 5) + 2]));
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
-    const uint32_t u1 = kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
+    const uint32_t u1 = kTab == 4 ? HPK_L4_HELD(e1) : kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
     const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
     if (kDup == 1) {
         const volatile HPK_LDS_AS uint32_t* vl = (const volatile HPK_LDS_AS uint32_t*)lut;
         asm volatile("" ::"v"(vl[w >> (32 - HPK_LUT_BITS)]));
         asm volatile("" ::"v"(vl[(w << u1) >> (32 - HPK_LUT_BITS)]));
     }
-    const uint32_t u2 = kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
-    const uint32_t o1 = L.o + (kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1));
+    const uint32_t u2 = kTab == 4 ? HPK_L4_HELD(e2) : kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
+    const uint32_t o1 = L.o + (kTab == 4 ? HPK_L4_C8(e1) >> 3 : kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1));
     if (kStore != kNoStore) {
         if (kDup == 3) {
             volatile HPK_LDS_AS uint8_t* v8 = (volatile HPK_LDS_AS uint8_t*)out8;
             v8[L.o] = (uint8_t)e1;
-            (v8 + 1)[L.o] = (uint8_t)(e1 >> 16);
+            (v8 + 1)[L.o] = (uint8_t)lut_sym1<kTab>(e1);
             v8[o1] = (uint8_t)e2;
-            (v8 + 1)[o1] = (uint8_t)(e2 >> 16);
+            (v8 + 1)[o1] = (uint8_t)lut_sym1<kTab>(e2);
         }
         out8[L.o] = (uint8_t)e1;
-        (out8 + 1)[L.o] = (uint8_t)(e1 >> 16);
+        (out8 + 1)[L.o] = (uint8_t)lut_sym1<kTab>(e1);
         out8[o1] = (uint8_t)e2;
-        (out8 + 1)[o1] = (uint8_t)(e2 >> 16);
+        (out8 + 1)[o1] = (uint8_t)lut_sym1<kTab>(e2);
     }
-    L.o = o1 + (kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2));
+    L.o = o1 + (kTab == 4 ? HPK_L4_C8(e2) >> 3 : kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2));
     const uint32_t xn = L.X + u1 + u2;
     const bool cross = (xn ^ L.X) > 31u;
     L.d0 = cross ? L.d1 : L.d0;
@@ -430,6 +442,97 @@ __device__ __forceinline__ void lit_or_step(Lit12& L, const uint32_t* __restrict
     L.prog = a1 | park;
     L.more = park | more2;
     if (park) lit_or_long(L, win32, lo, img32);
+}
+
+// ------------------------------------------------------------------------------------------
+// Accumulated dword output (decode v32, the wave kernel's body steps in fills whose output regions
+// all start and end on 4-byte boundaries, as hpk_decoded_bound rounded up to 4 makes them). A step's
+// decoded bytes (up to four, LUT4: zero above the codes an entry holds) are shifted into the lane's
+// pending dword (L.pe1: the bytes of the dword holding the output position, zero from it on); the dword
+// is stored, whole and aligned, by the step that completes it, and every other step stores it to the
+// lane's dummy slot (no exec-mask branch). One ds_write_b32 per step replaces four ds_write_b8: the
+// byte stores were ~45 % of the body's LDS bank-conflict cycles (profiles/r04/lds_attribution/), and a
+// dword store to a random address costs what a byte store does. L.o is the output position in BITS
+// (8 x the LDS byte address) while the body runs. A dword the step completes lies inside the literal's
+// region: it ends at or before the output position, which stays below the region's end. acc_flush
+// stores the part-filled dword at the body's end, before the checked tail steps store bytes over its
+// upper part; the dword lies inside the region because the region's end is 4-aligned and above the
+// output position (>= 5 bits are left after a body step, so the decoded length stays below the
+// decoded bound). Semantics are lit12_body's (huffman.rs:95-161); only the stores differ.
+#ifndef HPK_ACC_PIPE
+#define HPK_ACC_PIPE 1
+#endif
+__device__ __forceinline__ void acc_put(Lit12& L, uint32_t v, uint32_t c8, uint8_t* __restrict__ out8, uint32_t dmy) {
+    const uint64_t t = (uint64_t)v << (L.o & 24u);
+    const uint32_t lo = L.acc | (uint32_t)t;
+    const uint32_t on = L.o + c8;
+    const bool full = (on ^ L.o) > 31u;  // (c8 <= 32: the dword at L.o is complete)
+    *reinterpret_cast<uint32_t*>(out8 + (full ? (L.o >> 3) & ~3u : dmy)) = lo;
+    L.acc = full ? (uint32_t)(t >> 32) : lo;
+    L.o = on;
+}
+// (HPK_ACC_PIPE) the bytes of the previous body step's entries (pe1, pe2; zero entries: nothing)
+__device__ __forceinline__ void acc_pend(Lit12& L, uint8_t* __restrict__ out8, uint32_t dmy) {
+    acc_put(L, (L.pe1 & 0xFFFFu) | ((L.pe2 & 0xFFFFu) << HPK_L4_C8(L.pe1)), HPK_L4_C8(L.pe1) + HPK_L4_C8(L.pe2), out8, dmy);
+    L.pe1 = L.pe2 = 0u;
+}
+__device__ __forceinline__ void acc_flush(Lit12& L, uint8_t* __restrict__ out8, uint32_t dmy) {
+#if HPK_ACC_PIPE
+    acc_pend(L, out8, dmy);
+#endif
+    if (L.o & 24u) *reinterpret_cast<uint32_t*>(out8 + ((L.o >> 3) & ~3u)) = L.acc;
+    L.o >>= 3;
+    L.acc = 0u;
+}
+__device__ __forceinline__ void lit_acc_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, uint32_t dmy,
+                                             bool& body) {
+    const uint32_t d3 = win32[(L.X >> 5) + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
+#if HPK_ACC_PIPE  // the previous step's bytes while this step's first lookup is in flight
+    HPK_SCHED_FENCE();
+    acc_pend(L, out8, dmy);
+    HPK_SCHED_FENCE();
+#endif
+    const uint32_t u1 = HPK_L4_HELD(e1);
+    const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
+    const uint32_t u2 = HPK_L4_HELD(e2);
+    const uint32_t xn = L.X + u1 + u2;
+    const bool cross = (xn ^ L.X) > 31u;
+    L.d0 = cross ? L.d1 : L.d0;
+    L.d1 = cross ? L.d2 : L.d1;
+    L.d2 = cross ? d3 : L.d2;
+    L.X = xn;
+#if HPK_ACC_PIPE
+    L.pe1 = e1;
+    L.pe2 = e2;
+#else
+    acc_put(L, (e1 & 0xFFFFu) | ((e2 & 0xFFFFu) << HPK_L4_C8(e1)), HPK_L4_C8(e1) + HPK_L4_C8(e2), out8, dmy);
+#endif
+    if (u2 == 0u) {
+#if HPK_ACC_PIPE
+        acc_pend(L, out8, dmy);
+#endif  // e2 holds no code (nor e1, if u1 == 0): a 13..30-bit code or EOS at X with > 12 bits
+                     // left (lit12_body)
+        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+        uint32_t sy, len;
+        bool eos;
+        lo_decode(wp, lo, sy, len, eos);
+        const uint32_t r = L.Eb - L.X;
+        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+            L.st = HPK_PADDING_TOO_LARGE;
+            L.Eb = L.X;
+        } else if (eos) {  // huffman.rs:112-116
+            L.st = HPK_EOS_IN_STRING;
+            L.Eb = L.X;
+        } else {
+            acc_put(L, sy, 8u, out8, dmy);
+            L.X += len;
+            lit12_load(L, win32);
+        }
+    }
+    body = L.Eb - L.X >= kBodyMin;
 }
 
 }  // namespace hpkdec

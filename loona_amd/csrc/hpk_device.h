@@ -101,7 +101,8 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b);
 // The compacted mode: b.out_off is the bound layout made by hpk_bound_scan, co_off the caller's output
 // offsets, cursor the (zeroed) output cursor, long_list the slot's long-literal list (the caller took the
 // slot with hpk_long_list and records it used after its last operation on the stream).
-int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor);
+int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor,
+                              int* wave);
 // out[i] = sum over j < i of the 4-rounded decoded bound of literal j (n + 1 entries), on the ctx
 // stream; tmp == nullptr: *tmp_bytes = the scratch it needs.
 int hpk_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out, void* tmp, size_t* tmp_bytes);

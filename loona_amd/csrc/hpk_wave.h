@@ -32,6 +32,8 @@
 //     read at every fill, the workgroup's other waves at their next fill.
 // Semantics are huffman.rs:95-161 through lit12_step (hpk_decode12.h).
 #pragma once
+#include <type_traits>
+
 #include "hpk_decode12.h"
 
 
@@ -43,6 +45,11 @@
 #endif
 #ifndef HPK_LUT3
 #define HPK_LUT3 1  // v28: the wave kernel's lookups in the LUT3 layout (byte-wide "bits held")
+#endif
+#ifndef HPK_WAVE_ACC
+#define HPK_WAVE_ACC 0  // 1: body steps of fills with 4-aligned regions store one accumulated dword per step
+                        // (lit_acc_body, LUT4) instead of four bytes: measured 847-863 us against 804-821
+                        // (round 5, profiles/r05/ab_acc_dword_*rejected.jsonl, software-pipelined or not)
 #endif
 #ifndef HPK_WAVE_OR
 #define HPK_WAVE_OR 0  // 1: fills decode into a zeroed image by dword ORs (lit_or_body / lit_or_step, LUT4):
@@ -72,10 +79,30 @@ struct GeoW {
 // WG counters (s_ctr): [0] bad offsets seen (waves stop at their next fill), [1] long list, front
 // (>= long_big bytes), [2] long list, back, [3] long-phase claim, [4]/[5] dense check sums, [6] the
 // dense listing found an entry it cannot list, [7] chunks of kChunk literals handed out to the waves,
-// [8] huge literals listed (s_huge = s_ctr + 16, at most kHugeMax of them; hpk_huge.h)
+// [8] huge literals listed (s_huge = s_ctr + 16, at most kHugeMax of them; hpk_huge.h), [9] (kCompact) bytes
+// of the workgroup's bound span handed out
 // kRank: 0 = counting sort with LDS atomics on 32 length classes of 2 bytes, 1 / 2 = ranks from
 // ballots over 16 classes of 4 bytes / 32 classes of 2 bytes (no LDS round trip)
-template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank>
+// Inclusive sum over the wave's 64 lanes: DPP row shifts within rows of 16 lanes (zero fill), then the
+// rows' totals by readlane.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    return x + (lane >= 16u ? r0 : 0u) + (lane >= 32u ? r1 : 0u) + (lane >= 48u ? r2 : 0u);
+}
+
+// kCompact (hpk_decode_batch_compact, round 5): a.out_off is the library's bound layout (4-rounded
+// decoded bounds); each workgroup packs its output into its own range's bound span [out_off[BA],
+// out_off[BB]) from an LDS cursor (s_ctr[9]): every decoded fill takes its decoded total there and is
+// gathered into it (compact_fill), every listed literal takes its 4-rounded bound there when it is
+// listed (co_off). No device-wide cursor: one atomic per fill on one word would be ~290k per 32M-literal
+// launch, against the ~88 per us one word takes (MI355X_MICROARCH.md, dequeue).
+template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank, bool kCompact = false>
 __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     using G = GeoW<kWinB, kImgB>;
     constexpr int kStore = kMode == 2 ? kNoStore : kPred;
@@ -111,8 +138,12 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     // v31: the fills' steps OR whole dwords into a zeroed image (LUT4); the long and huge phases get
     // the LUT3 / LUT2 layout back after the fills
     constexpr bool kOr = HPK_WAVE_OR && HPK_BODY && kMode != 1 && kMode != 2 && !(kMode >= 6 && kMode <= 10);
+    // v32: the fills' table is LUT4 (accumulated dword stores in 4-aligned fills, byte stores otherwise)
+    constexpr bool kAccOn = HPK_WAVE_ACC && HPK_BODY && !kOr && kMode != 1 && kMode != 2 && !(kMode >= 6 && kMode <= 10);
+    constexpr int kTabF = kAccOn ? 4 : kTab;
     for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
-        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kOr ? a.lut4 : kTab == 3 ? a.lut3 : a.lut2)[t];
+        reinterpret_cast<uint4*>(s_lut)[t] =
+            reinterpret_cast<const uint4*>(kOr || kAccOn ? a.lut4 : kTab == 3 ? a.lut3 : a.lut2)[t];
     if (tid < 16) s_ctr[tid] = 0;
     if (kMode == 3)
         for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
@@ -120,7 +151,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
+    const uint32_t wg0 = kCompact && BA < BB ? a.out_off[BA] : 0u;  // (kCompact) the range's bound span
     auto leave = [&](uint32_t i, uint32_t nb) {  // list literal i for the huge / long-literal phase
+        if (kCompact) a.co_off[i] = wg0 + atomicAdd(&s_ctr[9], ((nb * 8u) / 5u + 3u) & ~3u);
         if (nb >= HPK_HUGE_MIN && nb < kHugeLimit) {
             const uint32_t h = atomicAdd(&s_ctr[8], 1u);
             if (h < kHugeMax) {
@@ -174,6 +207,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     s_ctr[1] = 0;
                     s_ctr[2] = 0;
                     s_ctr[8] = 0;
+                    s_ctr[9] = 0;  // (kCompact: the listing's allocations are void)
                 }
                 __syncthreads();
             }
@@ -300,11 +334,126 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             }
             ri0 = ri1 = 0xFFFFFFFFu;
         };
+        // (kCompact) the decoded fill [fcur, fcur + fk) packed into the workgroup's span: its lengths in
+        // literal order (the window, dead once the fill is decoded, holds the tables), a wave scan, ONE
+        // LDS cursor add for the fill's total, offsets / lengths / statuses, then the destination in whole
+        // 16-byte chunks (the fill kernel's compact_flush, hpk_decode12.h): a map from each chunk to the
+        // literal holding its first byte, a chunk inside one literal made from five image dwords by
+        // alignbyte, one across literals byte by byte. q1 / q2: the lane's two queue entries (image offsets)
+        auto compact_fill = [&](uint32_t fcur, uint32_t fk, const uint2 q1, const uint2 q2) {
+            uint32_t* const s_len = reinterpret_cast<uint32_t*>(s_win);  // [128] len | status << 24, kListed
+            uint32_t* const s_pre = s_len + 128;                          // [129] exclusive prefix sums
+            uint32_t* const s_iof = s_pre + 132;                          // [128] image offsets
+            uint16_t* const s_map = reinterpret_cast<uint16_t*>(s_iof + 128);
+            static_assert((128 + 132 + 128) * 4 + (G::kImg / 16 + 2) * 2 <= kWinB, "compact tables in the window");
+            s_len[lane] = kListed;
+            s_len[lane + 64u] = kListed;
+            if (ri0 != 0xFFFFFFFFu) {
+                s_len[ri0] = rv0;
+                s_iof[ri0] = (q1.y >> 12) & 0x1FFFFu;
+            }
+            if (ri1 != 0xFFFFFFFFu) {
+                s_len[ri1] = rv1;
+                s_iof[ri1] = (q2.y >> 12) & 0x1FFFFu;
+            }
+            const uint32_t l0 = s_len[lane], l1 = s_len[lane + 64u];
+            const uint32_t x0 = l0 == kListed ? 0u : l0 & 0xFFFFFFu, x1 = l1 == kListed ? 0u : l1 & 0xFFFFFFu;
+            const uint32_t i0 = wave_incl_scan(x0, lane), i1 = wave_incl_scan(x1, lane);
+            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+            const uint32_t ex0 = i0 - x0, ex1 = t0 + i1 - x1;
+            const uint32_t tot = t0 + (uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
+            uint32_t u = 0;
+            if (lane == 0) u = atomicAdd(&s_ctr[9], tot);
+            const uint32_t base = wg0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)u);  // (blob-relative)
+            if (lane < fk && l0 != kListed) {
+                a.co_off[fcur + lane] = base + ex0;
+                a.out_len[fcur + lane] = x0;
+                a.status[fcur + lane] = (uint8_t)(l0 >> 24);
+            }
+            if (lane + 64u < fk && l1 != kListed) {
+                a.co_off[fcur + lane + 64u] = base + ex1;
+                a.out_len[fcur + lane + 64u] = x1;
+                a.status[fcur + lane + 64u] = (uint8_t)(l1 >> 24);
+            }
+#ifndef HPK_CW_DIAG
+#define HPK_CW_DIAG 0  // (measurement only) 1: no map and no gather, 2: the map but no gather, 3: no byte path
+#endif
+            if (tot == 0u || HPK_CW_DIAG == 1) return;
+            s_pre[lane] = ex0;
+            s_pre[lane + 64u] = ex1;
+            if (lane < 4u) s_pre[128u + lane] = tot;  // (the chunk reads look up to four literals ahead)
+            const uint32_t D0 = a.out_mis + base, D1 = D0 + tot, c0 = D0 >> 4;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
+                const uint32_t t = lane + 64u * r, ln = r ? x1 : x0;
+                const uint32_t d = D0 + (r ? ex1 : ex0), e = d + ln;
+                if (ln) {
+                    const uint32_t clo = d == D0 ? c0 : (d + 15u) >> 4;
+                    for (uint32_t c = clo; c <= ((e - 1u) >> 4); ++c) s_map[c - c0] = (uint16_t)t;
+                }
+            }
+            if (HPK_CW_DIAG == 2) return;
+            const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_img);
+            // image bytes [a, a + 4) as a dword (little-endian), a any alignment
+            // (clamped into the image: the chunk reads also make the addresses of literals they do not take,
+            // from stale or absent s_iof entries)
+            auto udw = [&](uint32_t a) {
+                a = min(a, (uint32_t)kImgB - 8u);
+                return __builtin_amdgcn_alignbyte(img32[(a >> 2) + 1u], img32[a >> 2], a & 3u);
+            };
+            for (uint32_t c = c0 + lane; c < ((D1 + 15u) >> 4); c += 64u) {
+                const uint32_t x0c = max(c << 4, D0), x1c = min((c << 4) + 16u, D1);
+                // the literal holding the chunk's first byte (i) and the next three: their starts p[k]
+                // (prefix sums, relative to D0) and image offsets of their byte j (so[k] + j), read at
+                // once (three LDS round trips per chunk: the map, these, the image dwords)
+                const uint32_t i = s_map[c - c0];
+                uint32_t p[5], so[4];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) p[k] = s_pre[i + k];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) so[k] = s_iof[i + k] - p[k];
+                if (x0c == (c << 4) && x1c == (c << 4) + 16u) {
+                    // a whole chunk, dword by dword: a dword inside one literal is one unaligned image dword,
+                    // one across two literals two merged (bfi); more literals in a chunk, bytes below
+                    uint32_t v[4];
+                    bool slow = false;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t d = (c << 4) + 4u * (uint32_t)q - D0;
+                        const uint32_t kd = (uint32_t)(d >= p[1]) + (uint32_t)(d >= p[2]) + (uint32_t)(d >= p[3]);
+                        const uint32_t ke = (uint32_t)(d + 3u >= p[1]) + (uint32_t)(d + 3u >= p[2]) + (uint32_t)(d + 3u >= p[3]);
+                        slow |= (d + 3u >= p[4]) | (ke > kd + 1u);
+                        const uint32_t sa = kd == 0 ? so[0] : kd == 1 ? so[1] : kd == 2 ? so[2] : so[3];
+                        const uint32_t sb = kd == 0 ? so[1] : kd == 1 ? so[2] : so[3];
+                        const uint32_t pb = kd == 0 ? p[1] : kd == 1 ? p[2] : p[3];  // where the next literal starts
+                        const uint32_t wa = udw(sa + d), wb = udw(sb + d);
+                        const uint32_t m = ke == kd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu << (8u * (pb - d)));  // bytes of wa
+                        v[q] = (wa & m) | (wb & ~m);
+                    }
+                    if (!slow) {
+                        reinterpret_cast<uint4*>(a.out_base)[c] = make_uint4(v[0], v[1], v[2], v[3]);
+                        continue;
+                    }
+                }
+                // the fill's first and last chunk (partial), or one holding more literals: byte by byte
+                if (HPK_CW_DIAG == 3) continue;
+                uint32_t ii = i, bn = p[1], ss = so[0];
+                for (uint32_t x = x0c; x < x1c; ++x) {
+                    const uint32_t j = x - D0;
+                    while (j >= bn) {  // (empty and listed literals: equal prefix sums)
+                        ++ii;
+                        bn = s_pre[ii + 1];
+                        ss = s_iof[ii] - s_pre[ii];
+                    }
+                    a.out_base[x] = s_img[ss + j];
+                }
+            }
+        };
         while (cur < ce) {  // wave-uniform
             const uint32_t cntl = min(128u, ce - cur);
             const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
             // 1. offsets: bounds (bad), what fits
-            bool bad = false;
+            bool bad = false, unal = false;
             uint32_t ex[2], ey[2];
             bool fits[2];
 #pragma unroll
@@ -314,12 +463,14 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const uint32_t p0 = io0[r] + a.in_mis, p1 = io1[r] + a.in_mis;
                 const uint32_t o0 = oo0[r] + a.out_mis, o1 = oo1[r] + a.out_mis;
                 fits[r] = t < cntl && p1 - base16 <= (uint32_t)kWinB && o1 - ob16 <= (uint32_t)G::kImg;
+                unal |= fits[r] && ((o0 | o1) & 3u) != 0u;
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
                 const bool fast = ocap >= (nbytes * 8u) / 5u;
                 ex[r] = (p0 - base16) | (nbytes << 16);
                 ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
             }
             const bool wbad = __any(bad) || stop != 0u;
+            const bool fal = kAccOn && !__any(unal);  // every region of the fill 4-aligned (wave-uniform)
             stamp(1);
             dg_add(8, 1u);
             if (wbad) {  // the rest of the wave's chunks is void; nothing more is decoded or written here
@@ -353,6 +504,11 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     } else {
                         const GlobalSrc g{reinterpret_cast<const uint32_t*>(a.in_base), last16 * 4 + 3};
                         uint8_t* dst = a.out_base + gout;
+                        if (kCompact) {  // (never with the library's bound layout: such a literal is listed)
+                            const uint32_t o = wg0 + atomicAdd(&s_ctr[9], ((nb * 8u) / 5u + 3u) & ~3u);
+                            a.co_off[cur] = o;
+                            dst = a.out_base + a.out_mis + o;
+                        }
                         Lit L = {};
                         lit_bytes_to(L, g, s_lo, [&](uint32_t j, uint8_t v) { dst[j] = v; },
                                      a.out_off[cur + 1] - a.out_off[cur], gin, a.in_off[cur + 1] + a.in_mis - gin);
@@ -485,6 +641,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 T.st = HPK_OK;
                 T.prog = false;
                 T.pe1 = T.pe2 = 0u;
+                T.acc = 0u;
                 lit12_load(T, wl32);
             };
             load(L, e1, t1);
@@ -498,77 +655,96 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 // v27: body steps (lit12_body, no fit tests) while a literal has >= kBodyMin bits left,
                 // slot t1's body then slot t2's; then the checked steps (lit12_step) for the two
                 // literals' last bits, t1's tail then t2's. A lane's first literal waits between the
-                // two phases as (aX, aO, aSt).
-                bool body = L.Eb - L.X >= kBodyMin;
-                uint32_t aX = L.X, aO = L.o, aSt = L.st;
-                bool aAct = L.act, onA = true;
-                for (;;) {
-                    dg_add(9, 1u);
+                // two phases as (aX, aO, aSt). v32 (kA, fills whose regions are all 4-aligned): the body
+                // steps store accumulated dwords (lit_acc_body; L.o in bits while the body runs, the
+                // part-filled dword stored by acc_flush when it ends)
+                auto bodywalk = [&](auto acc_tag) {
+                    constexpr bool kA = decltype(acc_tag)::value;
+                    bool body = L.Eb - L.X >= kBodyMin;
+                    if (kA) L.o <<= 3;
+                    uint32_t aX = L.X, aO = L.o, aSt = L.st;
+                    bool aAct = L.act, onA = true;
+                    for (;;) {
+                        dg_add(9, 1u);
 #pragma unroll
-                    for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
-                        if (body && kOr)
-                            lit_or_body(L, wl32, s_lut, s_lo, img32, body);
-                        else if (body)
-                            lit12_body<kStore, kTab, (kMode >= 8 && kMode <= 10) ? kMode - 7 : 0>(L, wl32, s_lut, s_lo,
-                                                                                                   ol8, body);
-                        if (kMode == 6) {
+                        for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
+                            if (body && kOr)
+                                lit_or_body(L, wl32, s_lut, s_lo, img32, body);
+                            else if (body && kA)
+                                lit_acc_body(L, wl32, s_lut, s_lo, ol8, dmy, body);
+                            else if (body)
+                                lit12_body<kStore, kTabF, (kMode >= 8 && kMode <= 10) ? kMode - 7 : 0>(L, wl32, s_lut, s_lo,
+                                                                                                        ol8, body);
+                            if (kMode == 6) {
 #pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[0]) : "v"(L.X));
-                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[1]) : "v"(L.o));
-                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[2]) : "v"(L.Eb));
-                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[3]) : "v"(L.d1));
+                                for (int q = 0; q < 4; ++q) {
+                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[0]) : "v"(L.X));
+                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[1]) : "v"(L.o));
+                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[2]) : "v"(L.Eb));
+                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[3]) : "v"(L.d1));
+                                }
                             }
                         }
-                    }
-                    if (__any(!body)) {
-                        const bool sw = !body & onA;
-                        if (sw) {  // the first literal's body is done: it waits, the second one starts (its
-                                   // state made from the queue entry here, not carried through the loop)
-                            if (kOr) lit_or_pend(L, img32);
-                            aX = L.X;
-                            aO = L.o;
-                            aSt = L.st;
-                            aAct = L.act;
-                            load(L, e2, t2);
-                            onA = false;
-                            body = L.Eb - L.X >= kBodyMin;
+                        if (__any(!body)) {
+                            const bool sw = !body & onA;
+                            if (sw) {  // the first literal's body is done: it waits, the second one starts (its
+                                       // state made from the queue entry here, not carried through the loop)
+                                if (kOr) lit_or_pend(L, img32);
+                                if (kA) acc_flush(L, ol8, dmy);
+                                aX = L.X;
+                                aO = L.o;
+                                aSt = L.st;
+                                aAct = L.act;
+                                load(L, e2, t2);
+                                if (kA) L.o <<= 3;
+                                onA = false;
+                                body = L.Eb - L.X >= kBodyMin;
+                            }
+                            if (!__any(body)) break;
                         }
-                        if (!__any(body)) break;
                     }
-                }
-                // tails: both literals of the lane at once, t1's from where its body stopped (restored
-                // into L), t2's (in N) from where its body stopped; a step that proves the walk has
-                // ended clears `more`, so no step is spent finding out (usually one step per tail)
-                if (kOr) lit_or_pend(L, img32);
-                N = L;
-                L.X = aX;
-                L.o = aO;
-                L.st = aSt;
-                L.act = aAct;
-                L.Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (aAct ? (e1.x >> 16) * 8u : 0u);
-                L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);  // (bytes; L.o in bits when kOr)
-                L.idx = e1.y & 0xFFFu;
-                if (aSt != HPK_OK) L.Eb = L.X;  // ended in its body (EOS / padding): no tail
-                lit12_load(L, wl32);
-                L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
-                N.more = N.Eb - N.X >= 5u;
-                while (__any(L.more | N.more)) {
-                    if (kOr) {
-                        if (L.more) lit_or_step(L, wl32, s_lut, s_lo, img32);
-                        if (N.more) lit_or_step(N, wl32, s_lut, s_lo, img32);
-                    } else {
-                        if (L.more) lit12_step<kStore, true, kTab, true>(L, wl32, s_lut, s_lo, ol8, dmy);
-                        if (N.more) lit12_step<kStore, true, kTab, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                    // tails: both literals of the lane at once, t1's from where its body stopped (restored
+                    // into L), t2's (in N) from where its body stopped; a step that proves the walk has
+                    // ended clears `more`, so no step is spent finding out (usually one step per tail)
+                    if (kOr) lit_or_pend(L, img32);
+                    if (kA) acc_flush(L, ol8, dmy);
+                    N = L;
+                    L.X = aX;
+                    L.o = aO;
+                    L.st = aSt;
+                    L.act = aAct;
+                    L.Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (aAct ? (e1.x >> 16) * 8u : 0u);
+                    L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);  // (bytes; L.o in bits when kOr)
+                    L.idx = e1.y & 0xFFFu;
+                    if (aSt != HPK_OK) L.Eb = L.X;  // ended in its body (EOS / padding): no tail
+                    lit12_load(L, wl32);
+                    L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
+                    N.more = N.Eb - N.X >= 5u;
+                    while (__any(L.more | N.more)) {
+                        if (kOr) {
+                            if (L.more) lit_or_step(L, wl32, s_lut, s_lo, img32);
+                            if (N.more) lit_or_step(N, wl32, s_lut, s_lo, img32);
+                        } else {
+                            if (L.more) lit12_step<kStore, true, kTabF, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                            if (N.more) lit12_step<kStore, true, kTabF, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                        }
                     }
+                    // results in the v26 form: the first slot's end state saved, the second in L
+                    sX = L.X;
+                    sO = kOr ? L.o >> 3 : L.o;
+                    sSt = L.st;
+                    s1 = L.act;
+                    L = N;
+                    Lend = kOr ? L.o >> 3 : L.o;
+                };
+                if constexpr (kAccOn) {
+                    if (fal)
+                        bodywalk(std::integral_constant<bool, true>{});
+                    else
+                        bodywalk(std::integral_constant<bool, false>{});
+                } else {
+                    bodywalk(std::integral_constant<bool, false>{});
                 }
-                // results in the v26 form: the first slot's end state saved, the second in L
-                sX = L.X;
-                sO = kOr ? L.o >> 3 : L.o;
-                sSt = L.st;
-                s1 = L.act;
-                L = N;
-                Lend = kOr ? L.o >> 3 : L.o;
             } else if (kMode != 1) {
                 for (;;) {
                     dg_add(9, 1u);
@@ -645,10 +821,21 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 }
             }
             stamp(7);
-            pk = k;
-            pcur = cur;
-            pG0 = gout;
-            pG1 = gout_end;
+            if (kCompact) {
+                // the next fill's prefetched offsets and window are waited for HERE (they landed during the
+                // lane loop): waited for after compact_fill, the wait (vmcnt counts loads and stores in
+                // issue order) would cover every store of the fill's write-back
+#pragma unroll
+                for (int r = 0; r < 2; ++r) asm volatile("" ::"v"(io0[r]), "v"(io1[r]), "v"(oo0[r]), "v"(oo1[r]));
+#pragma unroll
+                for (int r = 0; r < R; ++r) asm volatile("" ::"v"(ch[r].x), "v"(ch[r].y), "v"(ch[r].z), "v"(ch[r].w));
+                compact_fill(cur, k, e1, e2);
+            } else {
+                pk = k;
+                pcur = cur;
+                pG0 = gout;
+                pG1 = gout_end;
+            }
             cur = cur_n;
             ce = ce_n;
             gin = gin_n;
@@ -660,7 +847,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     // ---- the literals left to the long-literal phase ----
     __syncthreads();  // every wave's fills, list entries and stores are out
     const uint32_t c1 = s_ctr[1], c2 = s_ctr[2], nh = min(s_ctr[8], kHugeMax);
-    if (kOr && c1 + c2 + nh != 0u) {  // (block-uniform) the phases' table layout
+    if ((kOr || kAccOn) && c1 + c2 + nh != 0u) {  // (block-uniform) the phases' table layout
         for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
             reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
         __syncthreads();

@@ -36,6 +36,10 @@ if [ "$KIND" = asan ] || [ "$KIND" = all ]; then
 fi
 if [ "$KIND" = tsan ] || [ "$KIND" = all ]; then
   build tsan "-fsanitize=thread"
-  run tsan libtsan.so TSAN_OPTIONS=halt_on_error=1:exitcode=66:report_signal_unsafe=0
+  # (left out under TSan, run under ASan/UBSan: the tests that fork or spawn — test_block_decoder_after_fork,
+  # tests/test_shard.py's gloo process groups, tests/test_walk_emulation.py and tests/test_tables.py: compiler and emulator
+  # subprocesses: a child forked from the multi-threaded pytest process hangs under the TSan runtime
+  # before it execs, whatever the library does)
+  PYTEST_ARGS="$PYTEST_ARGS --deselect tests/test_hpack.py::test_block_decoder_after_fork --ignore tests/test_shard.py --ignore tests/test_walk_emulation.py --ignore tests/test_tables.py" run tsan libtsan.so TSAN_OPTIONS=halt_on_error=1:exitcode=66:report_signal_unsafe=0
 fi
 echo "sanitizers: clean"

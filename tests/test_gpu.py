@@ -15,19 +15,19 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module", params=["fill", "wave", "compact"])
+@pytest.fixture(scope="module", params=["fill", "wave", "compact", "compact_wave"])
 def codec(request):
     """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the
     workgroup fills and the wave fills) and in the compacted-output form (hpk_decode_batch_compact,
-    through gpu_decode / _device_decode; tests that pass their own output regions run the fill kernel
-    there), which must all give identical results."""
+    through gpu_decode / _device_decode) under each kernel (tests that pass their own output regions
+    run the region form of that kernel there), which must all give identical results."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a GPU (run with -m 'not gpu' on CPU)")
     from loona_amd import HuffmanCodec
 
     c = HuffmanCodec(0, stream=torch.cuda.current_stream())
-    c.set_decode_kernel("fill" if request.param == "compact" else request.param)
-    c.compact = request.param == "compact"
+    c.set_decode_kernel({"compact": "fill", "compact_wave": "wave"}.get(request.param, request.param))
+    c.compact = request.param.startswith("compact")
     yield c
     c.close()
 
