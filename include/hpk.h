@@ -121,10 +121,14 @@ int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
  * out_blob[out_off[i] .. out_off[i] + out_len[i]) and out_off[n] is the end of everything written.
  * out_off (n+1 entries) is an OUTPUT here. Literals are packed in runs (a fill of the kernel at a
  * time, literal order inside a run, runs in completion order), so out_off is not monotone. A literal
- * the kernel hands to its long- or huge-literal phase keeps a region of its decoded bound, the bytes
- * past its out_len unwritten: every literal of >= 64 encoded bytes, and every literal (short ones
- * too) of a workgroup range the kernel lists whole because most of its input bytes are in such
- * literals.
+ * the kernel hands to its long- or huge-literal phase keeps a region of its 4-rounded decoded bound,
+ * the bytes past its out_len unwritten: every literal of >= 64 encoded bytes, and every literal
+ * (short ones too) of a workgroup range the kernel lists whole because most of its input bytes are
+ * in such literals. Batches the wave-fill kernel decodes (>= 4M literals, or that kernel forced by
+ * hpk_ctx_set_decode_kernel) are packed per workgroup: each workgroup's runs and listed regions
+ * fill its literal range's share of the bound layout (the 4-rounded decoded bounds back to back)
+ * from its start, the rest of that share unwritten, and out_off[n] is the bound layout's end; the
+ * workgroup-fill kernel packs every run from one device cursor and out_off[n] is its end.
  * Device pointers only (HPK_PTR_DEVICE, optionally HPK_ASYNC); out_cap must be at least
  * hpk_decoded_bound(in_cap) + 4 * n (HPK_E_INVAL otherwise). Statuses, errors and offsets checks
  * as hpk_decode_batch. */

@@ -319,6 +319,79 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
     body = L.Eb - L.X >= kBodyMin;
 }
 
+// Two literals' body steps in one block (decode v32, the wave kernel): a lane's two literals L and N
+// step together, each while its body flag holds; a chain whose body has ended stands still (no advance)
+// and stores to the lane's dummy slot. One wave's instructions issue in order, so a step alone waits out
+// its two dependent table reads (~150 cycles each with the bank conflicts of 64 random addresses;
+// bench/step_probe.hip: the bare chain 398 cycles per step, the product step 638, one wave on an idle
+// CU); two independent chains in one block fill each other's waits. The byte stores and the long-code
+// branch are lit12_body's, chain by chain; semantics are lit12_body's (huffman.rs:95-161).
+template <int kStore, int kTab = 2>
+__device__ __forceinline__ void lit12_body2(Lit12& L, Lit12& N, const uint32_t* __restrict__ win32,
+                                            const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo,
+                                            uint8_t* __restrict__ out8, uint32_t dmy, bool& bl, bool& bn) {
+    auto held = [](uint32_t e) { return kTab == 3 ? HPK_L3_HELD(e) : HPK_L2_HELD(e); };
+    auto codes = [](uint32_t e) { return kTab == 3 ? HPK_L3_CODES(e) : HPK_L2_CODES(e); };
+    const uint32_t dL = win32[(L.X >> 5) + 2], dN = win32[(N.X >> 5) + 2];
+    const uint32_t wL = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X), wN = __builtin_amdgcn_alignbit(N.d0, N.d1, ~N.X);
+    const uint32_t eL1 = lut[wL >> (32 - HPK_LUT_BITS)], eN1 = lut[wN >> (32 - HPK_LUT_BITS)];
+    const uint32_t uL1 = held(eL1), uN1 = held(eN1);
+    const uint32_t eL2 = lut[(wL << uL1) >> (32 - HPK_LUT_BITS)], eN2 = lut[(wN << uN1) >> (32 - HPK_LUT_BITS)];
+    const uint32_t uL2 = held(eL2), uN2 = held(eN2);
+    // stores (an ended chain's to the dummy slot: its bytes past the output position may lie past its
+    // region), then the advance (none for an ended chain)
+    const uint32_t oL1 = L.o + codes(eL1), oN1 = N.o + codes(eN1);
+    if (kStore != kNoStore) {
+        const uint32_t aL = bl ? L.o : dmy, aL1 = bl ? oL1 : dmy, aN = bn ? N.o : dmy, aN1 = bn ? oN1 : dmy;
+        out8[aL] = (uint8_t)eL1;
+        (out8 + 1)[aL] = (uint8_t)(eL1 >> 16);
+        out8[aL1] = (uint8_t)eL2;
+        (out8 + 1)[aL1] = (uint8_t)(eL2 >> 16);
+        out8[aN] = (uint8_t)eN1;
+        (out8 + 1)[aN] = (uint8_t)(eN1 >> 16);
+        out8[aN1] = (uint8_t)eN2;
+        (out8 + 1)[aN1] = (uint8_t)(eN2 >> 16);
+    }
+    L.o = bl ? oL1 + codes(eL2) : L.o;
+    N.o = bn ? oN1 + codes(eN2) : N.o;
+    const uint32_t xL = L.X + (bl ? uL1 + uL2 : 0u), xN = N.X + (bn ? uN1 + uN2 : 0u);
+    const bool cL = (xL ^ L.X) > 31u, cN = (xN ^ N.X) > 31u;
+    L.d0 = cL ? L.d1 : L.d0;
+    L.d1 = cL ? L.d2 : L.d1;
+    L.d2 = cL ? dL : L.d2;
+    N.d0 = cN ? N.d1 : N.d0;
+    N.d1 = cN ? N.d2 : N.d1;
+    N.d2 = cN ? dN : N.d2;
+    L.X = xL;
+    N.X = xN;
+    const bool pL = bl & (uL2 == 0u), pN = bn & (uN2 == 0u);
+    if (pL | pN) {  // a 13..30-bit code or EOS (lit12_body's leading-ones branch), chain by chain
+        auto park = [&](Lit12& T) {
+            const uint32_t wp = __builtin_amdgcn_alignbit(T.d0, T.d1, ~T.X);
+            uint32_t sy, len;
+            bool eos;
+            lo_decode(wp, lo, sy, len, eos);
+            const uint32_t r = T.Eb - T.X;
+            if (len > r) {  // huffman.rs:128-134
+                T.st = HPK_PADDING_TOO_LARGE;
+                T.Eb = T.X;
+            } else if (eos) {  // huffman.rs:112-116
+                T.st = HPK_EOS_IN_STRING;
+                T.Eb = T.X;
+            } else {
+                if (kStore != kNoStore) out8[T.o] = (uint8_t)sy;
+                T.o += 1;
+                T.X += len;
+                lit12_load(T, win32);
+            }
+        };
+        if (pL) park(L);
+        if (pN) park(N);
+    }
+    bl = bl & (L.Eb - L.X >= kBodyMin);
+    bn = bn & (N.Eb - N.X >= kBodyMin);
+}
+
 // Final status of a literal whose walk has stopped; a status set by the walk wins.
 __device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
     if (L.st != HPK_OK) return L.st;

@@ -51,6 +51,13 @@
                         // (lit_acc_body, LUT4) instead of four bytes: measured 847-863 us against 804-821
                         // (round 5, profiles/r05/ab_acc_dword_*rejected.jsonl, software-pipelined or not)
 #endif
+#ifndef HPK_WAVE_DUAL
+#define HPK_WAVE_DUAL 0  // 1: a lane's two literals' body steps in one block (lit12_body2): bit-exact (GPU suite
+                         // 176 passed) but 1098-1105 us against 810-814 (round 5, profiles/r05/ab_dual_walk_rejected.jsonl)
+#endif
+#ifndef HPK_DUAL_UNROLL
+#define HPK_DUAL_UNROLL 2  // fused double steps between the wave's end checks
+#endif
 #ifndef HPK_WAVE_OR
 #define HPK_WAVE_OR 0  // 1: fills decode into a zeroed image by dword ORs (lit_or_body / lit_or_step, LUT4):
                        // measured 882-899 us against 855-870 (round 5, profiles/r05/ab_or_output_rejected.jsonl)
@@ -342,12 +349,16 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         // alignbyte, one across literals byte by byte. q1 / q2: the lane's two queue entries (image offsets)
         auto compact_fill = [&](uint32_t fcur, uint32_t fk, const uint2 q1, const uint2 q2) {
             uint32_t* const s_len = reinterpret_cast<uint32_t*>(s_win);  // [128] len | status << 24, kListed
-            uint32_t* const s_pre = s_len + 128;                          // [129] exclusive prefix sums
-            uint32_t* const s_iof = s_pre + 132;                          // [128] image offsets
-            uint16_t* const s_map = reinterpret_cast<uint16_t*>(s_iof + 128);
-            static_assert((128 + 132 + 128) * 4 + (G::kImg / 16 + 2) * 2 <= kWinB, "compact tables in the window");
+            uint32_t* const s_iof = s_len + 128;                          // [128] image offsets
+            // [133] per literal (its exclusive prefix sum p, the image offset of its byte j = so + j);
+            // entries 128..132 past the fill: (tot, 0)
+            uint2* const s_rec = reinterpret_cast<uint2*>(s_iof + 128);
+            uint16_t* const s_map = reinterpret_cast<uint16_t*>(s_rec + 134);
+            static_assert((128 + 128 + 2 * 134) * 4 + (G::kImg / 16 + 2) * 2 <= kWinB, "compact tables in the window");
             s_len[lane] = kListed;
             s_len[lane + 64u] = kListed;
+            s_iof[lane] = 0u;
+            s_iof[lane + 64u] = 0u;
             if (ri0 != 0xFFFFFFFFu) {
                 s_len[ri0] = rv0;
                 s_iof[ri0] = (q1.y >> 12) & 0x1FFFFu;
@@ -357,6 +368,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 s_iof[ri1] = (q2.y >> 12) & 0x1FFFFu;
             }
             const uint32_t l0 = s_len[lane], l1 = s_len[lane + 64u];
+            const uint32_t f0 = s_iof[lane], f1 = s_iof[lane + 64u];
             const uint32_t x0 = l0 == kListed ? 0u : l0 & 0xFFFFFFu, x1 = l1 == kListed ? 0u : l1 & 0xFFFFFFu;
             const uint32_t i0 = wave_incl_scan(x0, lane), i1 = wave_incl_scan(x1, lane);
             const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
@@ -365,23 +377,30 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             uint32_t u = 0;
             if (lane == 0) u = atomicAdd(&s_ctr[9], tot);
             const uint32_t base = wg0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)u);  // (blob-relative)
-            if (lane < fk && l0 != kListed) {
-                a.co_off[fcur + lane] = base + ex0;
-                a.out_len[fcur + lane] = x0;
-                a.status[fcur + lane] = (uint8_t)(l0 >> 24);
-            }
-            if (lane + 64u < fk && l1 != kListed) {
-                a.co_off[fcur + lane + 64u] = base + ex1;
-                a.out_len[fcur + lane + 64u] = x1;
-                a.status[fcur + lane + 64u] = (uint8_t)(l1 >> 24);
-            }
+            // offsets, lengths, statuses: stored last (a spill reload in between waits for every older
+            // vector-memory operation, these stores included)
+            auto results = [&]() {
+                if (lane < fk && l0 != kListed) {
+                    a.co_off[fcur + lane] = base + ex0;
+                    a.out_len[fcur + lane] = x0;
+                    a.status[fcur + lane] = (uint8_t)(l0 >> 24);
+                }
+                if (lane + 64u < fk && l1 != kListed) {
+                    a.co_off[fcur + lane + 64u] = base + ex1;
+                    a.out_len[fcur + lane + 64u] = x1;
+                    a.status[fcur + lane + 64u] = (uint8_t)(l1 >> 24);
+                }
+            };
 #ifndef HPK_CW_DIAG
 #define HPK_CW_DIAG 0  // (measurement only) 1: no map and no gather, 2: the map but no gather, 3: no byte path
 #endif
-            if (tot == 0u || HPK_CW_DIAG == 1) return;
-            s_pre[lane] = ex0;
-            s_pre[lane + 64u] = ex1;
-            if (lane < 4u) s_pre[128u + lane] = tot;  // (the chunk reads look up to four literals ahead)
+            if (tot == 0u || HPK_CW_DIAG == 1) {
+                results();
+                return;
+            }
+            s_rec[lane] = make_uint2(ex0, f0 - ex0);
+            s_rec[lane + 64u] = make_uint2(ex1, f1 - ex1);
+            if (lane < 6u) s_rec[128u + lane] = make_uint2(tot, 0u);  // (the chunk reads look ahead)
             const uint32_t D0 = a.out_mis + base, D1 = D0 + tot, c0 = D0 >> 4;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
@@ -392,62 +411,69 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     for (uint32_t c = clo; c <= ((e - 1u) >> 4); ++c) s_map[c - c0] = (uint16_t)t;
                 }
             }
-            if (HPK_CW_DIAG == 2) return;
+            if (HPK_CW_DIAG == 2) {
+                results();
+                return;
+            }
             const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_img);
-            // image bytes [a, a + 4) as a dword (little-endian), a any alignment
-            // (clamped into the image: the chunk reads also make the addresses of literals they do not take,
-            // from stale or absent s_iof entries)
-            auto udw = [&](uint32_t a) {
-                a = min(a, (uint32_t)kImgB - 8u);
-                return __builtin_amdgcn_alignbyte(img32[(a >> 2) + 1u], img32[a >> 2], a & 3u);
-            };
+            // (image addresses are clamped into the image: the reads below also address literals a chunk
+            // does not take)
             for (uint32_t c = c0 + lane; c < ((D1 + 15u) >> 4); c += 64u) {
                 const uint32_t x0c = max(c << 4, D0), x1c = min((c << 4) + 16u, D1);
-                // the literal holding the chunk's first byte (i) and the next three: their starts p[k]
-                // (prefix sums, relative to D0) and image offsets of their byte j (so[k] + j), read at
-                // once (three LDS round trips per chunk: the map, these, the image dwords)
+                // the literal holding the chunk's first byte (i) and the next two: where they start
+                // (relative to D0) and their image offsets (byte j at so + j)
                 const uint32_t i = s_map[c - c0];
-                uint32_t p[5], so[4];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) p[k] = s_pre[i + k];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) so[k] = s_iof[i + k] - p[k];
+                const uint2 ra = s_rec[i], rb = s_rec[i + 1], rc = s_rec[i + 2], rd = s_rec[i + 3];
+                // (read together: left to itself the compiler sank each read into the branch using it, one
+                // LDS round trip after another)
+                asm volatile("" ::"v"(ra.x), "v"(ra.y), "v"(rb.x), "v"(rb.y), "v"(rc.x), "v"(rd.x));
                 if (x0c == (c << 4) && x1c == (c << 4) + 16u) {
-                    // a whole chunk, dword by dword: a dword inside one literal is one unaligned image dword,
-                    // one across two literals two merged (bfi); more literals in a chunk, bytes below
-                    uint32_t v[4];
-                    bool slow = false;
+                    // a whole chunk: five image dwords of literal i and five of literal i + 1 (the chunk's
+                    // bytes at their offsets), each output dword from one of them or merged across the
+                    // boundary; a chunk reaching a third literal (one of < 16 bytes) goes bytewise
+                    const uint32_t d0 = (c << 4) - D0;
+                    const uint32_t aa = min(ra.y + d0, (uint32_t)kImgB - 20u), ab = min(rb.y + d0, (uint32_t)kImgB - 20u);
+                    uint32_t A[5], B[5];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t d = (c << 4) + 4u * (uint32_t)q - D0;
-                        const uint32_t kd = (uint32_t)(d >= p[1]) + (uint32_t)(d >= p[2]) + (uint32_t)(d >= p[3]);
-                        const uint32_t ke = (uint32_t)(d + 3u >= p[1]) + (uint32_t)(d + 3u >= p[2]) + (uint32_t)(d + 3u >= p[3]);
-                        slow |= (d + 3u >= p[4]) | (ke > kd + 1u);
-                        const uint32_t sa = kd == 0 ? so[0] : kd == 1 ? so[1] : kd == 2 ? so[2] : so[3];
-                        const uint32_t sb = kd == 0 ? so[1] : kd == 1 ? so[2] : so[3];
-                        const uint32_t pb = kd == 0 ? p[1] : kd == 1 ? p[2] : p[3];  // where the next literal starts
-                        const uint32_t wa = udw(sa + d), wb = udw(sb + d);
-                        const uint32_t m = ke == kd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu << (8u * (pb - d)));  // bytes of wa
-                        v[q] = (wa & m) | (wb & ~m);
+                    for (int j = 0; j < 5; ++j) {
+                        A[j] = img32[(aa >> 2) + (uint32_t)j];
+                        B[j] = img32[(ab >> 2) + (uint32_t)j];
                     }
-                    if (!slow) {
-                        reinterpret_cast<uint4*>(a.out_base)[c] = make_uint4(v[0], v[1], v[2], v[3]);
-                        continue;
+                    if (d0 + 16u <= rc.x || rc.x == rd.x && d0 + 16u <= rd.x) {
+                        // (an empty literal i + 2 with i + 3 past the chunk: the same two literals)
+                        const uint32_t pb = rb.x;  // where literal i + 1 starts
+                        uint32_t v[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t d = d0 + 4u * (uint32_t)q;
+                            const uint32_t wa = __builtin_amdgcn_alignbyte(A[q + 1], A[q], aa & 3u);
+                            const uint32_t wb = __builtin_amdgcn_alignbyte(B[q + 1], B[q], ab & 3u);
+                            // bytes of wa: all below pb (none when d >= pb)
+                            const uint32_t m = d + 4u <= pb ? 0xFFFFFFFFu : d >= pb ? 0u : ~(0xFFFFFFFFu << (8u * (pb - d)));
+                            v[q] = (wa & m) | (wb & ~m);
+                        }
+                        if (pb == ra.x || pb == rc.x) {  // (an empty literal i or i + 1: bytewise, below)
+                        } else {
+                            reinterpret_cast<uint4*>(a.out_base)[c] = make_uint4(v[0], v[1], v[2], v[3]);
+                            continue;
+                        }
                     }
                 }
                 // the fill's first and last chunk (partial), or one holding more literals: byte by byte
                 if (HPK_CW_DIAG == 3) continue;
-                uint32_t ii = i, bn = p[1], ss = so[0];
+                uint32_t ii = i, bn = rb.x, ss = ra.y;
                 for (uint32_t x = x0c; x < x1c; ++x) {
                     const uint32_t j = x - D0;
                     while (j >= bn) {  // (empty and listed literals: equal prefix sums)
                         ++ii;
-                        bn = s_pre[ii + 1];
-                        ss = s_iof[ii] - s_pre[ii];
+                        const uint2 r2 = s_rec[ii], r3 = s_rec[ii + 1];
+                        bn = r3.x;
+                        ss = r2.y;
                     }
                     a.out_base[x] = s_img[ss + j];
                 }
             }
+            results();
         };
         while (cur < ce) {  // wave-uniform
             const uint32_t cntl = min(128u, ce - cur);
@@ -737,6 +763,36 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     L = N;
                     Lend = kOr ? L.o >> 3 : L.o;
                 };
+#if HPK_WAVE_DUAL
+                // v32: both literals' bodies stepped together (lit12_body2), then both tails
+                auto dualwalk = [&]() {
+                    load(N, e2, t2);
+                    bool bl = L.Eb - L.X >= kBodyMin, bn = N.Eb - N.X >= kBodyMin;
+                    while (__any(bl | bn)) {
+                        dg_add(9, 1u);
+#pragma unroll
+                        for (int s = 0; s < HPK_DUAL_UNROLL; ++s)
+                            lit12_body2<kStore, kTabF>(L, N, wl32, s_lut, s_lo, ol8, dmy, bl, bn);
+                    }
+                    if (L.st != HPK_OK) L.Eb = L.X;  // (ended in its body: no tail)
+                    if (N.st != HPK_OK) N.Eb = N.X;
+                    L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
+                    N.more = N.Eb - N.X >= 5u;
+                    while (__any(L.more | N.more)) {
+                        if (L.more) lit12_step<kStore, true, kTabF, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                        if (N.more) lit12_step<kStore, true, kTabF, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                    }
+                    sX = L.X;
+                    sO = L.o;
+                    sSt = L.st;
+                    s1 = L.act;
+                    L = N;
+                    Lend = L.o;
+                };
+                if (kMode == 0 || kMode == 3) {
+                    dualwalk();
+                } else
+#endif
                 if constexpr (kAccOn) {
                     if (fal)
                         bodywalk(std::integral_constant<bool, true>{});
