@@ -267,8 +267,11 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             ca = BA + (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
             ce = (uint32_t)__builtin_amdgcn_readfirstlane((int)ce);
         };
-        // registers of the next fill: offsets of slots lane and lane + 64, the window chunks
-        uint32_t io0[2], io1[2], oo0[2], oo1[2];
+        // registers of the next fill: the start offsets of slots lane and lane + 64 (a slot's end is the
+        // next slot's start, taken from the neighbouring lane by DPP at the fill's top: round 5, half the
+        // offset loads and four VGPRs fewer), the offsets of slot 128 (wave-uniform: scalar loads), the
+        // window chunks
+        uint32_t io0[2], oo0[2], ie = 0, oe = 0, pcnt = 1;
         uint4 ch[R];
         auto prefetch = [&](uint32_t c, uint32_t e, uint32_t base16) {
             const uint32_t cnt = min(128u, e - c);  // >= 1
@@ -276,13 +279,29 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = c + min(lane + 64u * r, cnt - 1u);
                 io0[r] = a.in_off[t];
-                io1[r] = a.in_off[t + 1];
                 oo0[r] = a.out_off[t];
-                oo1[r] = a.out_off[t + 1];
             }
+            ie = a.in_off[c + cnt];
+            oe = a.out_off[c + cnt];
+            pcnt = cnt;
             const uint4* g16 = reinterpret_cast<const uint4*>(a.in_base);
 #pragma unroll
             for (int r = 0; r < R; ++r) ch[r] = g16[min((base16 >> 4) + lane + 64u * r, last16)];
+        };
+        // the end offsets of the slots (wave_shl:1, lane i takes lane i + 1's value; lane 63 the next
+        // round's first, or slot 128's; a slot at or past the batch's last takes slot 128's)
+        uint32_t io1[2], oo1[2];
+        auto ends = [&]() {
+            const uint32_t i1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)io0[1]);
+            const uint32_t o1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)oo0[1]);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t ni = (uint32_t)__builtin_amdgcn_update_dpp((int)(r ? ie : i1), (int)io0[r], 0x130, 0xF, 0xF, false);
+                const uint32_t no = (uint32_t)__builtin_amdgcn_update_dpp((int)(r ? oe : o1), (int)oo0[r], 0x130, 0xF, 0xF, false);
+                const bool last = lane + 64u * r + 1u >= pcnt;
+                io1[r] = last ? ie : ni;
+                oo1[r] = last ? oe : no;
+            }
         };
         // A wave holds one chunk at a time and claims the next when its current one ends (its first
         // offsets are then loaded under the fill's setup): claimed a chunk ahead, the range's last
@@ -482,6 +501,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             bool bad = false, unal = false;
             uint32_t ex[2], ey[2];
             bool fits[2];
+            ends();
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = lane + 64u * r;
@@ -882,7 +902,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 // lane loop): waited for after compact_fill, the wait (vmcnt counts loads and stores in
                 // issue order) would cover every store of the fill's write-back
 #pragma unroll
-                for (int r = 0; r < 2; ++r) asm volatile("" ::"v"(io0[r]), "v"(io1[r]), "v"(oo0[r]), "v"(oo1[r]));
+                for (int r = 0; r < 2; ++r) asm volatile("" ::"v"(io0[r]), "v"(oo0[r]), "s"(ie), "s"(oe));
 #pragma unroll
                 for (int r = 0; r < R; ++r) asm volatile("" ::"v"(ch[r].x), "v"(ch[r].y), "v"(ch[r].z), "v"(ch[r].w));
                 compact_fill(cur, k, e1, e2);
