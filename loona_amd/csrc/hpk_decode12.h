@@ -148,23 +148,26 @@ __device__ __forceinline__ void lit12_load(Lit12& L, const uint32_t* __restrict_
 // going to the lane's dummy slot out8[dmy] (no exec-mask branch around each store); kChecked
 // (diagnostic mode 4) checks every store against the literal's capacity, kNoStore (mode 2) stores
 // nothing.
-template <int kStore, bool kP1 = false,   // kP1: a lookup's second byte stored at (address) + 1 by the
-          int kTab = 2,                  // store's offset (the wave kernel; in the fill kernel's
-          bool kMore = false>            // register budget the extra live dmy - 1 spills); kTab: lut12;
-                                         // kMore: set L.more (the tails of decode v27)
-__device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
-                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8,
-                                           uint32_t dmy = 0) {
+// (lit12_step's two parts: the lookups and their stores, returning whether a 13..30-bit code or EOS
+// starts at the new position; then that code's leading-ones lookup. on = false: the step does nothing
+// — no advance, its stores to the dummy slot — so two literals' steps can share one block, lit12_step2.)
+template <int kStore, bool kP1, int kTab, bool kMore>
+__device__ __forceinline__ bool lit12_step_main(Lit12& L, const uint32_t* __restrict__ win32,
+                                                const uint32_t* __restrict__ lut, uint8_t* __restrict__ out8,
+                                                uint32_t dmy, bool on = true) {
     const uint32_t d3 = win32[(L.X >> 5) + 2];  // the dword after d2, in case this step crosses one
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
     const uint32_t rem = L.Eb - L.X;
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
     bool a1, a2;
-    const uint32_t u1 = lut12<kTab>(e1, rem, a1, a2);
+    uint32_t u1 = lut12<kTab>(e1, rem, a1, a2);
+    a1 &= on;
+    a2 &= on;
+    u1 = on ? u1 : 0u;
     uint32_t use = u1;
     // a code longer than 12 bits (or EOS) starts here and may still fit (with more than 12 bits
     // left, any code the entry holds fits: no first code <=> the entry has none)
-    bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
+    bool park = on & !a1 & (rem > (uint32_t)HPK_LUT_BITS);
     bool more2 = false;
     if (kStore == kPred) {
         out8[a1 ? L.o : dmy] = (uint8_t)e1;
@@ -212,26 +215,61 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     L.X = xn;
     L.prog = a1 | park;
     if (kMore) L.more = park | more2;
-    if (park) {  // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
-        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-        uint32_t s, len;
-        bool eos;
-        lo_decode(wp, lo, s, len, eos);
-        const uint32_t r = L.Eb - L.X;
-        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
-            L.st = HPK_PADDING_TOO_LARGE;
-            L.Eb = L.X;
-            if (kMore) L.more = false;
-        } else if (eos) {  // huffman.rs:112-116
-            L.st = HPK_EOS_IN_STRING;
-            L.Eb = L.X;
-            if (kMore) L.more = false;
-        } else {
-            put8(out8, L.o, s, L.oend, kStore);
-            L.o += 1;
-            L.X += len;
-            lit12_load(L, win32);
-        }
+    return park;
+}
+
+template <int kStore, bool kMore>
+__device__ __forceinline__ void lit12_park(Lit12& L, const uint32_t* __restrict__ win32, const uint16_t* __restrict__ lo,
+                                           uint8_t* __restrict__ out8) {
+    // a 13..30-bit code or EOS: one leading-ones lookup (any code in one read)
+    const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
+    uint32_t s, len;
+    bool eos;
+    lo_decode(wp, lo, s, len, eos);
+    const uint32_t r = L.Eb - L.X;
+    if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
+        L.st = HPK_PADDING_TOO_LARGE;
+        L.Eb = L.X;
+        if (kMore) L.more = false;
+    } else if (eos) {  // huffman.rs:112-116
+        L.st = HPK_EOS_IN_STRING;
+        L.Eb = L.X;
+        if (kMore) L.more = false;
+    } else {
+        put8(out8, L.o, s, L.oend, kStore);
+        L.o += 1;
+        L.X += len;
+        lit12_load(L, win32);
+    }
+}
+
+// One step: two lookups (up to four codes of <= 12 bits) and, for a longer code, one leading-ones
+// lookup. kStore == kPred: the (up to) four byte stores are unconditional, a byte that is not output
+// going to the lane's dummy slot out8[dmy] (no exec-mask branch around each store); kChecked
+// (diagnostic mode 4) checks every store against the literal's capacity, kNoStore (mode 2) stores
+// nothing.
+template <int kStore, bool kP1 = false,   // kP1: a lookup's second byte stored at (address) + 1 by the
+          int kTab = 2,                  // store's offset (the wave kernel; in the fill kernel's
+          bool kMore = false>            // register budget the extra live dmy - 1 spills); kTab: lut12;
+                                         // kMore: set L.more (the tails of decode v27)
+__device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
+                                           const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8,
+                                           uint32_t dmy = 0) {
+    if (lit12_step_main<kStore, kP1, kTab, kMore>(L, win32, lut, out8, dmy)) lit12_park<kStore, kMore>(L, win32, lo, out8);
+}
+
+// The tails of a lane's two literals (HPK_TAIL2, off: measured slower): both checked steps in one block, each doing nothing
+// once its literal's walk has ended (more = false), so the two independent lookup chains share their
+// waits; the leading-ones lookups after both. Semantics are lit12_step's.
+template <int kStore, bool kP1, int kTab>
+__device__ __forceinline__ void lit12_step2(Lit12& L, Lit12& N, const uint32_t* __restrict__ win32,
+                                            const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo,
+                                            uint8_t* __restrict__ out8, uint32_t dmy) {
+    const bool pL = lit12_step_main<kStore, kP1, kTab, true>(L, win32, lut, out8, dmy, L.more);
+    const bool pN = lit12_step_main<kStore, kP1, kTab, true>(N, win32, lut, out8, dmy, N.more);
+    if (pL | pN) {
+        if (pL) lit12_park<kStore, true>(L, win32, lo, out8);
+        if (pN) lit12_park<kStore, true>(N, win32, lo, out8);
     }
 }
 

@@ -51,6 +51,10 @@
                         // (lit_acc_body, LUT4) instead of four bytes: measured 847-863 us against 804-821
                         // (round 5, profiles/r05/ab_acc_dword_*rejected.jsonl, software-pipelined or not)
 #endif
+#ifndef HPK_TAIL2
+#define HPK_TAIL2 0  // a lane's two tails stepped in one block (lit12_step2): measured slower, config 5
+                     // 810-821 vs 802-808 us (profiles/r05/ab_tail2_rejected.jsonl)
+#endif
 #ifndef HPK_WAVE_DUAL
 #define HPK_WAVE_DUAL 0  // 1: a lane's two literals' body steps in one block (lit12_body2): bit-exact (GPU suite
                          // 176 passed) but 1098-1105 us against 810-814 (round 5, profiles/r05/ab_dual_walk_rejected.jsonl)
@@ -770,6 +774,8 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                         if (kOr) {
                             if (L.more) lit_or_step(L, wl32, s_lut, s_lo, img32);
                             if (N.more) lit_or_step(N, wl32, s_lut, s_lo, img32);
+                        } else if (HPK_TAIL2) {  // both tails in one block (off)
+                            lit12_step2<kStore, true, kTabF>(L, N, wl32, s_lut, s_lo, ol8, dmy);
                         } else {
                             if (L.more) lit12_step<kStore, true, kTabF, true>(L, wl32, s_lut, s_lo, ol8, dmy);
                             if (N.more) lit12_step<kStore, true, kTabF, true>(N, wl32, s_lut, s_lo, ol8, dmy);
