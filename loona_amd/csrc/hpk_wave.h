@@ -51,6 +51,13 @@
                         // (lit_acc_body, LUT4) instead of four bytes: measured 847-863 us against 804-821
                         // (round 5, profiles/r05/ab_acc_dword_*rejected.jsonl, software-pipelined or not)
 #endif
+#ifndef HPK_CW_LANE
+#define HPK_CW_LANE 1  // v33: the compacted form's write-back by lane (each lane its two literals) instead
+                       // of the chunk gather (compact_fill)
+#endif
+#ifndef HPK_CW_LANE_DIAG
+#define HPK_CW_LANE_DIAG 0  // (measurement only) 2: no stores
+#endif
 #ifndef HPK_TAIL2
 #define HPK_TAIL2 0  // a lane's two tails stepped in one block (lit12_step2): measured slower, config 5
                      // 810-821 vs 802-808 us (profiles/r05/ab_tail2_rejected.jsonl)
@@ -113,6 +120,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 // gathered into it (compact_fill), every listed literal takes its 4-rounded bound there when it is
 // listed (co_off). No device-wide cursor: one atomic per fill on one word would be ~290k per 32M-literal
 // launch, against the ~88 per us one word takes (MI355X_MICROARCH.md, dequeue).
+// a dword and four dwords stored at any byte address (unaligned global stores)
+typedef uint32_t u32u __attribute__((aligned(1)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
 template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank, bool kCompact = false>
 __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     using G = GeoW<kWinB, kImgB>;
@@ -377,6 +388,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             // entries 128..132 past the fill: (tot, 0)
             uint2* const s_rec = reinterpret_cast<uint2*>(s_iof + 128);
             uint16_t* const s_map = reinterpret_cast<uint16_t*>(s_rec + 134);
+            uint32_t* const s_rec_ex = reinterpret_cast<uint32_t*>(s_rec);  // (HPK_CW_LANE)
             static_assert((128 + 128 + 2 * 134) * 4 + (G::kImg / 16 + 2) * 2 <= kWinB, "compact tables in the window");
             s_len[lane] = kListed;
             s_len[lane + 64u] = kListed;
@@ -421,10 +433,87 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 results();
                 return;
             }
+            const uint32_t D0 = a.out_mis + base, D1 = D0 + tot, c0 = D0 >> 4;
+#if HPK_CW_LANE
+            // (v33) each lane copies its own two slots' literals (the snake's long-with-short pair) from
+            // the image to their destinations in 16-byte stores at any byte alignment (the hardware's
+            // unaligned global accesses): a literal of n >= 16 bytes in pieces at 0, 16, ... and its last
+            // piece ending at n (rewriting some of its bytes with the same values), one of 4..15 bytes in
+            // dwords the same way, a shorter one bytewise; each stored dword from two image dwords by
+            // alignbyte; the pair's pieces in one loop
+            (void)D1;
+            (void)c0;
+            (void)f0;
+            (void)f1;
+            {
+                uint32_t* const s_ex = s_rec_ex;  // [128] exclusive prefix by literal index
+                s_ex[lane] = ex0;
+                s_ex[lane + 64u] = ex1;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_img);
+                uint32_t js[2], jd[2], jn[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t ri = r ? ri1 : ri0, rv = r ? rv1 : rv0;
+                    const bool on = ri != 0xFFFFFFFFu && rv != kListed;
+                    js[r] = ((r ? q2.y : q1.y) >> 12) & 0x1FFFFu;
+                    jd[r] = D0 + s_ex[on ? ri : 0u];
+                    jn[r] = on ? rv & 0xFFFFFFu : 0u;
+                }
+                // the image dword at byte u (any alignment)
+                auto dw_at = [&](uint32_t u) {
+                    return __builtin_amdgcn_alignbyte(img32[(u >> 2) + 1u], img32[u >> 2], u & 3u);
+                };
+                uint32_t sp = js[0], dp = jd[0], np = jn[0], tp = 0;
+                bool second = true;
+                if (np == 0u) {
+                    sp = js[1];
+                    dp = jd[1];
+                    np = jn[1];
+                    second = false;
+                }
+                while (HPK_CW_LANE_DIAG != 2 && __any(tp < np)) {
+                    if (tp < np) {
+                        if (np >= 16u) {  // a 16-byte piece at t (the last one ending at n)
+                            const uint32_t t = min(tp, np - 16u), u = sp + t;
+                            const uint32_t sw = u >> 2, s3 = u & 3u;
+                            uint32_t A[5];
+#pragma unroll
+                            for (int j = 0; j < 5; ++j) A[j] = img32[sw + (uint32_t)j];
+                            u32x4u v;
+                            v.x = __builtin_amdgcn_alignbyte(A[1], A[0], s3);
+                            v.y = __builtin_amdgcn_alignbyte(A[2], A[1], s3);
+                            v.z = __builtin_amdgcn_alignbyte(A[3], A[2], s3);
+                            v.w = __builtin_amdgcn_alignbyte(A[4], A[3], s3);
+                            *reinterpret_cast<u32x4u*>(a.out_base + dp + t) = v;
+                            tp += 16u;
+                        } else if (np >= 4u) {  // dwords at 0, 4, 8 and the last one ending at n
+                            u32u* const g = reinterpret_cast<u32u*>(a.out_base + dp);
+                            g[0] = dw_at(sp);
+                            if (np >= 8u) g[1] = dw_at(sp + 4u);
+                            if (np >= 12u) g[2] = dw_at(sp + 8u);
+                            *reinterpret_cast<u32u*>(a.out_base + dp + np - 4u) = dw_at(sp + np - 4u);
+                            tp = np;
+                        } else {
+                            for (uint32_t b = 0; b < np; ++b) a.out_base[dp + b] = s_img[sp + b];
+                            tp = np;
+                        }
+                        if (tp >= np && second) {
+                            sp = js[1];
+                            dp = jd[1];
+                            np = jn[1];
+                            tp = 0;
+                            second = false;
+                        }
+                    }
+                }
+            }
+            results();
+            return;
+#endif
             s_rec[lane] = make_uint2(ex0, f0 - ex0);
             s_rec[lane + 64u] = make_uint2(ex1, f1 - ex1);
             if (lane < 6u) s_rec[128u + lane] = make_uint2(tot, 0u);  // (the chunk reads look ahead)
-            const uint32_t D0 = a.out_mis + base, D1 = D0 + tot, c0 = D0 >> 4;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
                 const uint32_t t = lane + 64u * r, ln = r ? x1 : x0;
@@ -462,7 +551,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                         A[j] = img32[(aa >> 2) + (uint32_t)j];
                         B[j] = img32[(ab >> 2) + (uint32_t)j];
                     }
-                    if (d0 + 16u <= rc.x || rc.x == rd.x && d0 + 16u <= rd.x) {
+                    if (d0 + 16u <= rc.x || (rc.x == rd.x && d0 + 16u <= rd.x)) {
                         // (an empty literal i + 2 with i + 3 past the chunk: the same two literals)
                         const uint32_t pb = rb.x;  // where literal i + 1 starts
                         uint32_t v[4];
