@@ -125,10 +125,11 @@ int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
  * the bytes past its out_len unwritten: every literal of >= 64 encoded bytes, and every literal
  * (short ones too) of a workgroup range the kernel lists whole because most of its input bytes are
  * in such literals. Batches the wave-fill kernel decodes (>= 4M literals, or that kernel forced by
- * hpk_ctx_set_decode_kernel) are packed per workgroup: each workgroup's runs and listed regions
- * fill its literal range's share of the bound layout (the 4-rounded decoded bounds back to back)
- * from its start, the rest of that share unwritten, and out_off[n] is the bound layout's end; the
- * workgroup-fill kernel packs every run from one device cursor and out_off[n] is its end.
+ * hpk_ctx_set_decode_kernel) are packed per workgroup: workgroup w's runs and listed regions fill
+ * its literal range [a, b)'s share [U(a), U(b)) from its start, the rest of the share unwritten, where
+ * U(i) = floor(8 (in_off[i] - in_off[0]) / 5) + 4 i (it holds every 4-rounded decoded bound of the
+ * range), and out_off[n] = U(n); the workgroup-fill kernel packs every run from one device cursor and
+ * out_off[n] is its end.
  * Device pointers only (HPK_PTR_DEVICE, optionally HPK_ASYNC); out_cap must be at least
  * hpk_decoded_bound(in_cap) + 4 * n (HPK_E_INVAL otherwise). Statuses, errors and offsets checks
  * as hpk_decode_batch. */
@@ -340,6 +341,10 @@ void hpk_henc_out_free(hpk_henc_out* out);
  * Testing only: the calling thread's next n Huffman batches inside hpk_henc_encode_blocks fail
  * with HPK_E_DEVICE (n = 0 clears it), so that guarantee can be checked without a device fault. */
 void hpk_test_fail_batches(int n);
+/* Testing only: the compacted form's internal bound layout of n literals' device offsets in_off
+ * (n + 1 entries) into device memory out (n + 1 entries): the exclusive sum mod 2^32 of
+ * (floor(8 len / 5) + 3) & ~3, synchronously on the context's stream. */
+int hpk_test_bound_scan(hpk_ctx* ctx, const uint32_t* in_off, uint32_t n, uint32_t* out);
 
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);

@@ -80,6 +80,7 @@ EXPORTS = (
     "hpk_henc_encode_blocks",
     "hpk_henc_out_free",
     "hpk_test_fail_batches",
+    "hpk_test_bound_scan",
     "hpk_ctx_set_decode_kernel",
     "hpk_version",
 )
@@ -230,6 +231,8 @@ def lib() -> ctypes.CDLL:
         L.hpk_ctx_set_decode_kernel.restype = ctypes.c_int
         L.hpk_test_fail_batches.argtypes = [ctypes.c_int]
         L.hpk_test_fail_batches.restype = None
+        L.hpk_test_bound_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.hpk_test_bound_scan.restype = ctypes.c_int
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.33 gfx950 decode v33 (batches >= 4M literals: wave fills, each wave with its own LDS window and image, chunks by guided self-scheduling, longest-first queue, slot end offsets by DPP; below 4M: workgroup fills; fills and long-literal phase: body steps with no fit tests while >= 29 bits are left, then checked tails; long literals one lane each streaming from HBM after the fills; literals of >= 8 KiB by a whole workgroup in speculative pieces; compacted-output form: wave fills packed per workgroup from an LDS cursor, each lane storing its two literals in unaligned 16-byte pieces, workgroup fills from a device cursor); encode v4 (byte-balanced workgroup ranges, segmented scan, run accumulator, LDS image, live chunks only)"
+#define HPK_VERSION "hpk 0.34 gfx950 decode v34 (batches >= 4M literals: wave fills, each wave with its own LDS window and image, chunks by guided self-scheduling, longest-first queue, slot end offsets by DPP; below 4M: workgroup fills; fills and long-literal phase: body steps with no fit tests while >= 29 bits are left, then checked tails; long literals one lane each streaming from HBM after the fills; literals of >= 8 KiB by a whole workgroup in speculative pieces; compacted-output form: wave fills packed per workgroup from an LDS cursor into a bound layout made from the input offsets in the kernel, each lane storing its two literals in unaligned 16-byte pieces, workgroup fills from a device cursor); encode v4 (byte-balanced workgroup ranges, segmented scan, run accumulator, LDS image, live chunks only)"
 
 static thread_local std::string t_last_error;
 
@@ -424,10 +424,11 @@ extern "C" int hpk_decode_batch(hpk_ctx* c, const uint8_t* in_blob, size_t in_ca
                      flags);
 }
 
-// The compacted form (include/hpk.h): the fills' bound layout made on the device by a scan of the
-// literals' 4-rounded bounds (the kernel's images keep bound-sized regions: a literal's decoded length
-// is known only once it is decoded), the output cursor zeroed, the compacted-mode fill kernel, then the
-// cursor copied to out_off[n].
+// The compacted form (include/hpk.h). The kernels' images keep bound-sized regions (a literal's decoded
+// length is known only once it is decoded). Wave-fill kernel (large batches): it makes the bound layout
+// from in_off itself, each workgroup packing into its range's span, and writes out_off[n]. Workgroup-fill
+// kernel: the bound layout made on the device by a scan of the literals' 4-rounded bounds, the output
+// cursor zeroed, the kernel, then the cursor copied to out_off[n].
 extern "C" int hpk_decode_batch_compact(hpk_ctx* c, const uint8_t* in_blob, size_t in_cap, const uint32_t* in_off,
                                         uint32_t n, uint8_t* out_blob, size_t out_cap, uint32_t* out_off,
                                         uint32_t* out_len, uint8_t* status, int flags) {
@@ -447,6 +448,17 @@ extern "C" int hpk_decode_batch_compact(hpk_ctx* c, const uint8_t* in_blob, size
         int rc, j;
         uint32_t* ll = nullptr;
         if ((rc = hpk_long_list(c, n, &ll, &j))) return rc;
+        if (hpk_compact_wave(c, n)) {  // (the kernel makes its bound layout and writes out_off[n])
+            const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), nullptr, out_len,
+                              status};
+            if ((rc = hpk_launch_decode_compact(c, b, out_off, ll, nullptr, true))) return rc;
+            if ((rc = hpk_long_list_used(c, j))) return rc;
+            if (!(flags & HPK_ASYNC)) {
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                return take_err(c);
+            }
+            return HPK_E_OK;
+        }
         size_t tmp = 0;
         if ((rc = hpk_bound_scan(c, in_off, n, nullptr, nullptr, &tmp))) return rc;
         if (c->cp_bound_cap[j] < ((size_t)n + 1) * 4 || c->cp_tmp_cap[j] < tmp || !c->cp_cursor[j]) {
@@ -460,11 +472,9 @@ extern "C" int hpk_decode_batch_compact(hpk_ctx* c, const uint8_t* in_blob, size
         HIP_TRY(hipMemsetAsync(c->cp_cursor[j], 0, 4, c->stream));
         const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), c->cp_bound[j], out_len,
                           status};
-        int wave = 0;
-        if ((rc = hpk_launch_decode_compact(c, b, out_off, ll, c->cp_cursor[j], &wave))) return rc;
-        // the span written: the cursor (workgroup-fill kernel), or the bound layout's end (wave-fill kernel)
-        HIP_TRY(hipMemcpyAsync(out_off + n, wave ? c->cp_bound[j] + n : c->cp_cursor[j], 4, hipMemcpyDeviceToDevice,
-                               c->stream));
+        if ((rc = hpk_launch_decode_compact(c, b, out_off, ll, c->cp_cursor[j], false))) return rc;
+        // the span written: the cursor
+        HIP_TRY(hipMemcpyAsync(out_off + n, c->cp_cursor[j], 4, hipMemcpyDeviceToDevice, c->stream));
         if ((rc = hpk_long_list_used(c, j))) return rc;
     }
     if (!(flags & HPK_ASYNC)) {

@@ -24,7 +24,6 @@
 // code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
 #include <stdlib.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include "hpk_wave.h"
 
@@ -83,24 +82,151 @@ extern "C" int hpk_debug_stamps(unsigned long long* host, size_t cap_entries) {
 #endif
 
 namespace {
-// the 4-rounded decoded bound of literal i (0 past the end), for the compacted mode's bound layout
-struct BoundOf {
-    const uint32_t* off;
-    uint32_t n;
-    __host__ __device__ uint32_t operator()(uint32_t i) const {
-        if (i >= n) return 0u;
-        const uint64_t nb = (uint64_t)(off[i + 1] - off[i]);  // (decreasing offsets: the kernel reports them)
-        const uint64_t bd = ((nb * 8u) / 5u + 3u) & ~(uint64_t)3u;
-        return bd > 0x7FFFFFFFu ? 0x7FFFFFFFu : (uint32_t)bd;
+// The compacted mode's bound layout: the exclusive sum over the n + 1 elements "the 4-rounded decoded
+// bound of literal i" (0 for i = n; sums mod 2^32), in two passes over in_off: per 4,096-element tile the
+// sum of its bounds, one workgroup scanning the tile sums, then every tile scanned again with its base
+// (reads 2 x 4 B and writes 4 B per literal; hipcub's scan over a transform iterator took 151 us per
+// 32M literals, round 5).
+constexpr uint32_t kScanT = 256, kScanK = 16, kScanTile = kScanT * kScanK;
+
+__device__ __forceinline__ uint32_t bound_of(uint32_t a, uint32_t b) {
+    const uint64_t nb = (uint64_t)(b - a);  // (decreasing offsets: the decode kernel reports them)
+    const uint64_t bd = ((nb * 8u) / 5u + 3u) & ~(uint64_t)3u;
+    return bd > 0x7FFFFFFFu ? 0x7FFFFFFFu : (uint32_t)bd;
+}
+
+// the tile's offsets into LDS (striped, coalesced), element j's bound = s[j + 1] - s[j] (0 past n)
+__device__ __forceinline__ void scan_load(const uint32_t* __restrict__ off, uint32_t n, uint32_t base, uint32_t* s) {
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanK; ++k) {
+        const uint32_t j = base + t + kScanT * k;
+        s[t + kScanT * k] = j <= n ? off[j] : 0u;
     }
-};
+    if (t == 0) s[kScanTile] = base + kScanTile <= n ? off[base + kScanTile] : 0u;
+    __syncthreads();
+}
+
+// exclusive block scan of one value per thread (256 threads), total to *tot
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* s_w, uint32_t* tot) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63u) s_w[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kScanT / 64u; ++q) {
+        pre += q < w ? s_w[q] : 0u;
+        all += s_w[q];
+    }
+    *tot = all;
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(kScanT) void bound_tile_sums(const uint32_t* __restrict__ off, uint32_t n,
+                                                          uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s[kScanTile + 1];
+    __shared__ uint32_t s_w[kScanT / 64];
+    const uint32_t base = blockIdx.x * kScanTile, t = threadIdx.x;
+    scan_load(off, n, base, s);
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanK; ++k) {
+        const uint32_t l = t * kScanK + k;
+        acc += base + l < n ? bound_of(s[l], s[l + 1]) : 0u;
+    }
+    uint32_t tot;
+    (void)block_exscan(acc, s_w, &tot);
+    if (t == 0) sums[blockIdx.x] = tot;
+}
+
+// one workgroup: the tile sums' exclusive scan, in place
+__global__ __launch_bounds__(kScanT) void bound_sums_scan(uint32_t* __restrict__ sums, uint32_t nt) {
+    __shared__ uint32_t s_w[kScanT / 64];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nt; b0 += kScanT * kScanK) {
+        const uint32_t t = threadIdx.x;
+        uint32_t v[kScanK], acc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanK; ++k) {
+            const uint32_t j = b0 + t * kScanK + k;
+            v[k] = j < nt ? sums[j] : 0u;
+            acc += v[k];
+        }
+        uint32_t tot;
+        uint32_t x = carry + block_exscan(acc, s_w, &tot);
+#pragma unroll
+        for (uint32_t k = 0; k < kScanK; ++k) {
+            const uint32_t j = b0 + t * kScanK + k;
+            if (j < nt) sums[j] = x;
+            x += v[k];
+        }
+        carry += tot;
+        __syncthreads();  // (s_w reused)
+    }
+}
+
+__global__ __launch_bounds__(kScanT) void bound_tile_scan(const uint32_t* __restrict__ off, uint32_t n,
+                                                          const uint32_t* __restrict__ sums, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s[kScanTile + 1];
+    __shared__ uint32_t s_w[kScanT / 64];
+    const uint32_t base = blockIdx.x * kScanTile, t = threadIdx.x;
+    scan_load(off, n, base, s);
+    uint32_t v[kScanK], acc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanK; ++k) {
+        const uint32_t l = t * kScanK + k;
+        v[k] = base + l < n ? bound_of(s[l], s[l + 1]) : 0u;
+        acc += v[k];
+    }
+    uint32_t tot;
+    uint32_t x = sums[blockIdx.x] + block_exscan(acc, s_w, &tot);
+    __syncthreads();  // (every thread's bounds are read: the tile's offsets give way to its results)
+#pragma unroll
+    for (uint32_t k = 0; k < kScanK; ++k) {
+        s[t * kScanK + k] = x;
+        x += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kScanK; ++k) {
+        const uint32_t j = base + t + kScanT * k;
+        if (j <= n) out[j] = s[t + kScanT * k];
+    }
+}
 }  // namespace
 
 int hpk_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out, void* tmp, size_t* tmp_bytes) {
-    hipcub::CountingInputIterator<uint32_t> cnt(0u);
-    hipcub::TransformInputIterator<uint32_t, BoundOf, hipcub::CountingInputIterator<uint32_t>> it(cnt, BoundOf{in_off, n});
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, it, out, (int)n + 1, c->stream));
+    const uint32_t nt = (uint32_t)(((uint64_t)n + 1u + kScanTile - 1u) / kScanTile);  // tiles over n + 1 elements
+    if (!out) {
+        *tmp_bytes = (size_t)nt * 4u;
+        return HPK_E_OK;
+    }
+    if (*tmp_bytes < (size_t)nt * 4u) return HPK_E_INVAL;
+    uint32_t* sums = static_cast<uint32_t*>(tmp);
+    hipLaunchKernelGGL(bound_tile_sums, dim3(nt), dim3(kScanT), 0, c->stream, in_off, n, sums);
+    hipLaunchKernelGGL(bound_sums_scan, dim3(1), dim3(kScanT), 0, c->stream, sums, nt);
+    hipLaunchKernelGGL(bound_tile_scan, dim3(nt), dim3(kScanT), 0, c->stream, in_off, n, (const uint32_t*)sums, out);
+    HIP_TRY(hipGetLastError());
     return HPK_E_OK;
+}
+
+// (tests only) the bound layout of device offsets into device memory, synchronously
+extern "C" int hpk_test_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out) {
+    size_t tmp = 0;
+    int rc = hpk_bound_scan(c, in_off, n, nullptr, nullptr, &tmp);
+    if (rc) return rc;
+    void* t = nullptr;
+    HIP_TRY(hipMalloc(&t, tmp ? tmp : 4));
+    rc = hpk_bound_scan(c, in_off, n, out, t, &tmp);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    (void)hipFree(t);
+    return rc ? rc : e == hipSuccess ? HPK_E_OK : HPK_E_DEVICE;
 }
 
 static void decode_args(hpk_ctx* c, const hpk_batch& b, DecodeArgs& a) {
@@ -144,8 +270,12 @@ static uint32_t decode_blocks(hpk_ctx* c, const hpk_batch& b) {
 // The compacted form: the wave-fill kernel's (each workgroup packs into its range's bound span, no device
 // cursor: *wave = 1, out_off[n] is then the bound layout's end) for the batches the region form runs it
 // on, else the workgroup-fill kernel's (fills packed from the device cursor, *wave = 0)
+bool hpk_compact_wave(const hpk_ctx* c, uint32_t n) {
+    return c->decode_kernel == HPK_DECODE_WAVE || (c->decode_kernel == HPK_DECODE_AUTO && n >= HPK_WAVE_MIN);
+}
+
 int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor,
-                              int* wave) {
+                              bool wave) {
     DecodeArgs a;
     decode_args(c, b, a);
     a.lit_out = co_off;
@@ -154,8 +284,7 @@ int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, 
     a.long_list = long_list;
     a.long_min = HPK_LONG_MIN;
     a.long_big = HPK_LONG_BIG;
-    *wave = c->decode_kernel == HPK_DECODE_WAVE || (c->decode_kernel == HPK_DECODE_AUTO && b.n >= HPK_WAVE_MIN);
-    if (*wave) {
+    if (wave) {
         a.cursor = nullptr;  // (the huge phase takes a listed literal's region from co_off)
         hipLaunchKernelGGL((hpk_decode_wave<0, kWaveWin, kWaveImg, HPK_WAVE_CHUNK, HPK_WAVE_GUIDED, HPK_WAVE_RANK, true>),
                            dim3(decode_blocks(c, b)), dim3(Geo::kBlock), 0, c->stream, a);

@@ -98,11 +98,14 @@ int hpk_set_err_msg(const char* what, int code);
     } while (0)
 
 int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b);
-// The compacted mode: b.out_off is the bound layout made by hpk_bound_scan, co_off the caller's output
-// offsets, cursor the (zeroed) output cursor, long_list the slot's long-literal list (the caller took the
-// slot with hpk_long_list and records it used after its last operation on the stream).
+// The compacted mode, co_off the caller's output offsets, long_list the slot's long-literal list (the
+// caller took the slot with hpk_long_list and records it used after its last operation on the stream).
+// wave (hpk_compact_wave): the wave-fill kernel, which makes its bound layout from in_off itself and
+// writes co_off[n]; otherwise the workgroup-fill kernel, b.out_off the bound layout made by
+// hpk_bound_scan and cursor the (zeroed) output cursor.
+bool hpk_compact_wave(const hpk_ctx* c, uint32_t n);
 int hpk_launch_decode_compact(hpk_ctx* c, const hpk_batch& b, uint32_t* co_off, uint32_t* long_list, uint32_t* cursor,
-                              int* wave);
+                              bool wave);
 // out[i] = sum over j < i of the 4-rounded decoded bound of literal j (n + 1 entries), on the ctx
 // stream; tmp == nullptr: *tmp_bytes = the scratch it needs.
 int hpk_bound_scan(hpk_ctx* c, const uint32_t* in_off, uint32_t n, uint32_t* out, void* tmp, size_t* tmp_bytes);

@@ -173,7 +173,18 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
-    const uint32_t wg0 = kCompact && BA < BB ? a.out_off[BA] : 0u;  // (kCompact) the range's bound span
+    // (kCompact, v34) the bound layout is U(i) = floor(8 (in_off[i] - in_off[0]) / 5) + 4 i, made here
+    // from the input offsets (no scan, no out_off array): a literal's region U(i + 1) - U(i) holds its
+    // decoded bound, a range's span U(BB) - U(BA) every 4-rounded bound of its literals, and U(n) is
+    // hpk_decoded_bound(in_off[n] - in_off[0]) + 4 n (floor(8 d / 5) = d + 3 q + floor(3 r / 5), d = 5 q + r)
+    const uint32_t in0 = kCompact ? a.in_off[0] : 0u;
+    auto ulay = [&](uint32_t i, uint32_t io) -> uint32_t {
+        const uint32_t d = io - in0, q = __umulhi(d, 0xCCCCCCCDu) >> 2;
+        return d + 3u * q + (((d - 5u * q) * 39u) >> 6) + 4u * i;
+    };
+    auto oof = [&](uint32_t i) -> uint32_t { return kCompact ? ulay(i, a.in_off[i]) : a.out_off[i]; };
+    if (kCompact && blockIdx.x == 0 && tid == 0) a.co_off[a.n] = ulay(a.n, a.in_off[a.n]);  // the span's end
+    const uint32_t wg0 = kCompact && BA < BB ? oof(BA) : 0u;  // (kCompact) the range's bound span
     auto leave = [&](uint32_t i, uint32_t nb) {  // list literal i for the huge / long-literal phase
         if (kCompact) a.co_off[i] = wg0 + atomicAdd(&s_ctr[9], ((nb * 8u) / 5u + 3u) & ~3u);
         if (nb >= HPK_HUGE_MIN && nb < kHugeLimit) {
@@ -212,7 +223,8 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         if (s_ctr[4] > s_ctr[5] / 2u) {  // block-uniform
             bool no = false;
             for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
-                const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q0 = a.out_off[i], q1 = a.out_off[i + 1];
+                const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1];
+                const uint32_t q0 = kCompact ? ulay(i, p0) : a.out_off[i], q1 = kCompact ? ulay(i + 1u, p1) : a.out_off[i + 1];
                 const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
                                 (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
                 if (ok)
@@ -286,7 +298,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         // next slot's start, taken from the neighbouring lane by DPP at the fill's top: round 5, half the
         // offset loads and four VGPRs fewer), the offsets of slot 128 (wave-uniform: scalar loads), the
         // window chunks
-        uint32_t io0[2], oo0[2], ie = 0, oe = 0, pcnt = 1;
+        uint32_t io0[2], oo0[2], ie = 0, oe = 0, pcnt = 1, pc = 0;
         uint4 ch[R];
         auto prefetch = [&](uint32_t c, uint32_t e, uint32_t base16) {
             const uint32_t cnt = min(128u, e - c);  // >= 1
@@ -294,11 +306,12 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = c + min(lane + 64u * r, cnt - 1u);
                 io0[r] = a.in_off[t];
-                oo0[r] = a.out_off[t];
+                if (!kCompact) oo0[r] = a.out_off[t];  // (kCompact: made from io0 in ends())
             }
             ie = a.in_off[c + cnt];
-            oe = a.out_off[c + cnt];
+            if (!kCompact) oe = a.out_off[c + cnt];
             pcnt = cnt;
+            pc = c;
             const uint4* g16 = reinterpret_cast<const uint4*>(a.in_base);
 #pragma unroll
             for (int r = 0; r < R; ++r) ch[r] = g16[min((base16 >> 4) + lane + 64u * r, last16)];
@@ -307,6 +320,11 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         // round's first, or slot 128's; a slot at or past the batch's last takes slot 128's)
         uint32_t io1[2], oo1[2];
         auto ends = [&]() {
+            if (kCompact) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) oo0[r] = ulay(pc + min(lane + 64u * r, pcnt - 1u), io0[r]);
+                oe = ulay(pc + pcnt, ie);
+            }
             const uint32_t i1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)io0[1]);
             const uint32_t o1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)oo0[1]);
 #pragma unroll
@@ -327,7 +345,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         uint32_t sens[4] = {0u, 1u, 2u, 3u};  // diagnostic modes 6 / 7 only
         if (cur < ce) {
             gin = a.in_off[cur] + a.in_mis;
-            gout = a.out_off[cur] + a.out_mis;
+            gout = oof(cur) + a.out_mis;
             prefetch(cur, ce, gin & ~15u);
         }
         // the previous fill, not yet written back: literals [pcur, pcur + pk), output [pG0, pG1), and
@@ -636,7 +654,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 if (pk) flush();
                 pk = 0;
                 const uint32_t nb = a.in_off[cur + 1] - a.in_off[cur];
-                const bool left = nb >= a.long_min && a.out_off[cur + 1] - a.out_off[cur] >= (nb * 8u) / 5u;
+                const bool left = nb >= a.long_min && oof(cur + 1) - oof(cur) >= (nb * 8u) / 5u;
                 if (lane == 0) {
                     if (left) {
                         leave(cur, nb);
@@ -650,7 +668,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                         }
                         Lit L = {};
                         lit_bytes_to(L, g, s_lo, [&](uint32_t j, uint8_t v) { dst[j] = v; },
-                                     a.out_off[cur + 1] - a.out_off[cur], gin, a.in_off[cur + 1] + a.in_mis - gin);
+                                     oof(cur + 1) - oof(cur), gin, a.in_off[cur + 1] + a.in_mis - gin);
                         a.out_len[cur] = L.cnt;
                         a.status[cur] = (uint8_t)lit_status(L);
                     }
@@ -659,7 +677,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 if (cur == ce) claim(cur, ce);  // the next chunk
                 if (cur < ce) {
                     gin = a.in_off[cur] + a.in_mis;
-                    gout = a.out_off[cur] + a.out_mis;
+                    gout = oof(cur) + a.out_mis;
                     prefetch(cur, ce, gin & ~15u);
                 }
                 continue;
@@ -676,7 +694,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 claim(cur_n, ce_n);
                 if (cur_n < ce_n) {
                     gin_n = a.in_off[cur_n] + a.in_mis;
-                    gout_n = a.out_off[cur_n] + a.out_mis;
+                    gout_n = oof(cur_n) + a.out_mis;
                 }
             }
             // 2. the window, big-endian dwords: bit P of the stream is bit 31 - P % 32 of dword P / 32
@@ -981,7 +999,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     const uint32_t o = (e.y >> 12) & 0x1FFFFu;
                     Lit B = {};
                     lit_bytes_to(B, LdsSwapSrc{win32}, s_lo, [&](uint32_t j, uint8_t v) { s_img[o + j] = v; },
-                                 a.out_off[cur + i + 1] - a.out_off[cur + i], e.x & 0xFFFFu, e.x >> 16);
+                                 oof(cur + i + 1) - oof(cur + i), e.x & 0xFFFFu, e.x >> 16);
                     if (r == 0) {
                         rv0 = B.cnt | (lit_status(B) << 24);
                         ri0 = i;
@@ -997,7 +1015,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 // lane loop): waited for after compact_fill, the wait (vmcnt counts loads and stores in
                 // issue order) would cover every store of the fill's write-back
 #pragma unroll
-                for (int r = 0; r < 2; ++r) asm volatile("" ::"v"(io0[r]), "v"(oo0[r]), "s"(ie), "s"(oe));
+                for (int r = 0; r < 2; ++r) asm volatile("" ::"v"(io0[r]), "s"(ie));
 #pragma unroll
                 for (int r = 0; r < R; ++r) asm volatile("" ::"v"(ch[r].x), "v"(ch[r].y), "v"(ch[r].z), "v"(ch[r].w));
                 compact_fill(cur, k, e1, e2);

@@ -28,6 +28,7 @@ def codec(request):
     c = HuffmanCodec(0, stream=torch.cuda.current_stream())
     c.set_decode_kernel({"compact": "fill", "compact_wave": "wave"}.get(request.param, request.param))
     c.compact = request.param.startswith("compact")
+    c.variant = request.param
     yield c
     c.close()
 
@@ -1077,3 +1078,37 @@ def test_compact_two_streams_overlap(codec):
             for w, (out, oo, ol, st) in ((big, r1), (small, r2)):
                 _check_compact(out, oo, ol, w.n)
                 synth.check_decoded(w, out, oo, ol, st)
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, 4096, 4097, 300_001, 16_781_313])
+def test_bound_scan(codec, n):
+    """The compacted form's bound layout (hpk_bound_scan, two passes over in_off): the exclusive sum
+    of the literals' 4-rounded decoded bounds mod 2^32 over n + 1 elements, across the tile boundaries
+    (4,096 literals) and past one workgroup of tile sums (16,777,216 literals); decreasing offsets take
+    the clamped bound 2^31 - 1 rounded as the library does."""
+    import torch
+
+    from loona_amd import _lib
+
+    if codec.variant != "wave" and n > 4097:
+        pytest.skip("one kernel variant is enough for the large sizes")
+    g = np.random.default_rng(n + 11)
+    ln = g.integers(0, 80, size=n, dtype=np.int64)
+    if n > 100:
+        ln[g.integers(0, n, size=8)] = g.integers(2000, 5000, size=8)
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(ln, out=off[1:])
+    off32 = off.astype(np.uint32)
+    if n >= 4097:  # a decreasing pair: off[i + 1] - off[i] wraps in u32
+        off32[4000] = off32[4001] + 7
+    d = np.diff(off32.astype(np.int64)) % 2**32
+    b = np.minimum(((d * 8) // 5 + 3) & ~3, 0x7FFFFFFF)
+    want = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(b, out=want[1:])
+    want %= 2**32
+    din = torch.from_numpy(off32.view(np.int32)).to(codec.device)
+    dout = torch.full((n + 1,), -1, dtype=torch.int32, device=codec.device)
+    rc = _lib.lib().hpk_test_bound_scan(codec._h, din.data_ptr(), n, dout.data_ptr())
+    assert rc == 0
+    got = dout.cpu().numpy().view(np.uint32).astype(np.int64)
+    assert (got == want).all(), np.nonzero(got != want)[0][:5]
