@@ -241,8 +241,9 @@ def device_config2(codec, n=1_000_000, seed=SEED, device="cuda"):
                           desc=f"{n} short literals, decoded len U[8,64], fixture char model (device-generated)")
 
 
-def device_config3(codec, n=1_000_000, seed=SEED + 3, device="cuda"):
-    """Config-3 distribution (Zipf(1.1) lengths 8..4096, 5 % uniform bytes) made on the GPU."""
+def device_config3(codec, n=1_000_000, seed=SEED + 3, device="cuda", rnd=0.05):
+    """Config-3 distribution (Zipf(1.1) lengths 8..4096, 5 % uniform bytes) made on the GPU (rnd: the
+    uniform-bytes fraction, for measurements)."""
     import torch
 
     g = torch.Generator(device=device)
@@ -250,7 +251,7 @@ def device_config3(codec, n=1_000_000, seed=SEED + 3, device="cuda"):
     k = np.arange(8, 4097, dtype=np.float64)
     w = torch.tensor(1.0 / np.power(k - 7, 1.1), dtype=torch.float64, device=device)
     lens = torch.multinomial(w, n, replacement=True, generator=g) + 8
-    dec_blob, dec_off = _device_strings(g, lens, 0.05, device)
+    dec_blob, dec_off = _device_strings(g, lens, rnd, device)
     enc_blob, enc_off = _device_encode(codec, dec_blob, dec_off)
     return DeviceWorkload("config3", enc_blob, enc_off, dec_blob, dec_off,
                           desc=f"{n} mixed literals, Zipf(1.1) 8..4096, 5% uniform bytes (device-generated)")
