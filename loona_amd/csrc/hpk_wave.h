@@ -56,7 +56,8 @@
                        // of the chunk gather (compact_fill)
 #endif
 #ifndef HPK_CW_LANE_DIAG
-#define HPK_CW_LANE_DIAG 0  // (measurement only) 2: no stores
+#define HPK_CW_LANE_DIAG 0  // (measurement only) 2: no copy loop, 3: 16-byte pieces at 16-aligned
+                            // addresses, 4: no 16-byte stores
 #endif
 #ifndef HPK_TAIL2
 #define HPK_TAIL2 0  // a lane's two tails stepped in one block (lit12_step2): measured slower, config 5
@@ -503,7 +504,12 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                             v.y = __builtin_amdgcn_alignbyte(A[2], A[1], s3);
                             v.z = __builtin_amdgcn_alignbyte(A[3], A[2], s3);
                             v.w = __builtin_amdgcn_alignbyte(A[4], A[3], s3);
-                            *reinterpret_cast<u32x4u*>(a.out_base + dp + t) = v;
+                            if (HPK_CW_LANE_DIAG == 3)
+                                *reinterpret_cast<u32x4u*>(a.out_base + ((dp + t) & ~15u)) = v;
+                            else if (HPK_CW_LANE_DIAG == 4)
+                                asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+                            else
+                                *reinterpret_cast<u32x4u*>(a.out_base + dp + t) = v;
                             tp += 16u;
                         } else if (np >= 4u) {  // dwords at 0, 4, 8 and the last one ending at n
                             u32u* const g = reinterpret_cast<u32u*>(a.out_base + dp);
