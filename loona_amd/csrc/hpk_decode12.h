@@ -298,10 +298,14 @@ constexpr uint32_t kBodyMin = HPK_BODY_MIN;
 #ifndef HPK_LDS_AS
 #define HPK_LDS_AS __attribute__((address_space(3)))
 #endif
+#ifndef HPK_LAZY_D3
+#define HPK_LAZY_D3 0  // 1: the window dword after d2 read only by the lanes whose step crossed a dword (round 5:
+                       // config 5 781-789 vs 769-783 us, profiles/r05/ab_lazy_window_read_rejected.jsonl)
+#endif
 template <int kStore, int kTab = 2, int kDup = 0>
 __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
                                            const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, bool& body) {
-    const uint32_t d3 = win32[(L.X >> 5) + 2];
+    const uint32_t d3 = HPK_LAZY_D3 ? 0u : win32[(L.X >> 5) + 2];
     if (kDup == 2) asm volatile("" ::"v"(((const volatile HPK_LDS_AS uint32_t*)win32)[(L.X >> 5) + 2]));
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
@@ -332,7 +336,11 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
     const bool cross = (xn ^ L.X) > 31u;
     L.d0 = cross ? L.d1 : L.d0;
     L.d1 = cross ? L.d2 : L.d1;
-    L.d2 = cross ? d3 : L.d2;
+    if (HPK_LAZY_D3) {
+        if (cross) L.d2 = win32[(xn >> 5) + 1u];
+    } else {
+        L.d2 = cross ? d3 : L.d2;
+    }
     L.X = xn;
     if (u2 == 0u) {  // e2 holds no code (nor e1, if u1 == 0): a 13..30-bit code or EOS at X; > 12 bits are
                      // left (>= kBodyMin - 12 before this lookup), so the leading-ones branch of lit12_step applies
