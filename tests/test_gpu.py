@@ -1112,3 +1112,61 @@ def test_bound_scan(codec, n):
     assert rc == 0
     got = dout.cpu().numpy().view(np.uint32).astype(np.int64)
     assert (got == want).all(), np.nonzero(got != want)[0][:5]
+
+
+@pytest.mark.parametrize("shift", [1, 3, 6])
+def test_compact_unaligned_bases(codec, shift):
+    """The compacted form on blobs whose bases are not 16-, 4- or 2-aligned (the wave kernel's lane
+    stores are 16-byte pieces at any byte address, their last piece ending at the literal's last
+    byte): literals of 0-3 decoded bytes (bytewise), 4-15 (dwords), 16-100 (pieces) and >= 64 encoded
+    bytes (listed for the long-literal phase), a literal with bad padding; bytes equal the oracle's,
+    literals disjoint, nothing written outside [0, out_off[n]) of the output (guard bytes)."""
+    from hpk_util import oracle_encode
+
+    from loona_amd.batch import compact_capacity
+
+    if not codec.compact:
+        pytest.skip("the compacted form only")
+    g = np.random.default_rng(40 + shift)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, ABCDEFGH", np.uint8)
+    lits = []
+    for i in range(3000):
+        k = i % 10
+        n = int(g.integers(0, 4)) if k == 0 else int(g.integers(4, 16)) if k < 4 else \
+            int(g.integers(16, 101)) if k < 9 else int(g.integers(100, 400))
+        s = bytes(alpha[g.integers(0, alpha.size, size=n)])
+        if i % 97 == 5:
+            s = bytes(g.integers(0, 256, size=n, dtype=np.uint8))
+        e = oracle_encode(s)
+        if i % 101 == 7 and e:
+            e = e[:-1] + bytes([e[-1] & 0xF0])  # bad padding (or a changed last code)
+        lits.append(e)
+    blob, off = pack(lits)
+    n = len(lits)
+    want = oracle_decode_batch(blob, off)
+    guard = 4096
+    need = compact_capacity(blob.size, n)
+    ibig = torch.zeros(blob.size + 64, dtype=torch.uint8, device="cuda")
+    ibig[shift : shift + blob.size] = torch.from_numpy(blob).cuda()
+    din = ibig[shift : shift + blob.size]
+    big = torch.full((guard + need + guard + 16,), 0xAB, dtype=torch.uint8, device="cuda")
+    out = big[guard + shift : guard + shift + need]
+    oo = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    codec.decode_compact(din, to_dev(off.view(np.int32)), out, oo, ol, st, sync=True)
+    _check_compact(out, oo, ol, n)
+    gb = big.cpu().numpy()
+    assert (gb[: guard + shift] == 0xAB).all(), "bytes written before the output"
+    end = int(oo[n].item()) & 0xFFFFFFFF
+    assert (gb[guard + shift + end :] == 0xAB).all(), "bytes written past the reported span"
+    outn = gb[guard + shift : guard + shift + need]
+    oon = oo.cpu().numpy().view(np.uint32).astype(np.int64)
+    got = (outn, np.concatenate([oon[:n], [end]]), ol.cpu().numpy().view(np.uint32), st.cpu().numpy())
+    stw, lw = want[3], want[2]
+    assert (got[3] == stw).all(), np.nonzero(got[3] != stw)[0][:5]
+    assert (got[2] == lw).all(), np.nonzero(got[2] != lw)[0][:5]
+    wo = np.asarray(want[1], dtype=np.int64)
+    for i in range(n):
+        a, m = int(oon[i]), int(lw[i])
+        assert bytes(outn[a : a + m]) == bytes(want[0][wo[i] : wo[i] + m]), f"literal {i}"
