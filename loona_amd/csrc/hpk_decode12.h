@@ -41,6 +41,10 @@
 
 namespace hpkdec {
 
+// a dword and four dwords stored at any byte address (unaligned global stores: the compacted forms)
+typedef uint32_t u32u __attribute__((aligned(1)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
 // LDS carve-up: Geo7's regions plus a fifth counter (the long-literal queue head).
 template <int kWaves, int kW, int kO, int kQ>
 struct Geo12 : Geo7<kWaves, kW, kO, kQ, true> {
@@ -828,6 +832,9 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
 #ifndef HPK_COMPACT_STATIC
 #define HPK_COMPACT_STATIC 0
 #endif
+#ifndef HPK_CF_LANE
+#define HPK_CF_LANE 1  // round 5: lane stores of whole literals instead of the chunk gather
+#endif
 #ifndef HPK_COMPACT_NOCOPY
 #define HPK_COMPACT_NOCOPY 0  // (measurement only: no copy, no lengths)
 #endif
@@ -891,7 +898,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 s_pre[t] = exs[r];
                 const uint32_t ln = lenof(lst[r]);
                 const uint32_t d = D0 + exs[r], e = d + ln;
-                if (ln) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
+                if (!HPK_CF_LANE && ln) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
                     const uint32_t clo = d == D0 ? c0 : (d + 15u) >> 4;
                     for (uint32_t c = clo; c <= ((e - 1u) >> 4); ++c) s_map[c - c0] = (uint16_t)t;
                 }
@@ -905,6 +912,44 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         if (tid == 0) s_pre[fk] = carry;
         lds_barrier();
         const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_out);
+#if HPK_CF_LANE
+        // (round 5, as the wave kernel's compact_fill) each thread stores literals tid and tid + kBlock
+        // from the image in 16-byte pieces at any byte address, a literal's last piece ending at its
+        // last byte; 4..15 bytes in dwords the same way, fewer bytewise
+        (void)D1;
+        (void)c0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = tid + (uint32_t)G::kBlock * r;
+            const uint32_t np = t < fk && !HPK_COMPACT_NOCOPY ? lenof(lst[r]) : 0u;
+            const uint32_t sp = np ? s_iof[t] : 0u, dp = D0 + exs[r];
+            auto dw_at = [&](uint32_t u) {
+                return __builtin_amdgcn_alignbyte(img32[(u >> 2) + 1u], img32[u >> 2], u & 3u);
+            };
+            if (np >= 16u) {
+                for (uint32_t tp = 0; tp < np; tp += 16u) {
+                    const uint32_t tt = min(tp, np - 16u), u = sp + tt, sw = u >> 2, s3 = u & 3u;
+                    uint32_t A[5];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) A[j] = img32[sw + (uint32_t)j];
+                    u32x4u v;
+                    v.x = __builtin_amdgcn_alignbyte(A[1], A[0], s3);
+                    v.y = __builtin_amdgcn_alignbyte(A[2], A[1], s3);
+                    v.z = __builtin_amdgcn_alignbyte(A[3], A[2], s3);
+                    v.w = __builtin_amdgcn_alignbyte(A[4], A[3], s3);
+                    *reinterpret_cast<u32x4u*>(a.out_base + dp + tt) = v;
+                }
+            } else if (np >= 4u) {
+                u32u* const g = reinterpret_cast<u32u*>(a.out_base + dp);
+                g[0] = dw_at(sp);
+                if (np >= 8u) g[1] = dw_at(sp + 4u);
+                if (np >= 12u) g[2] = dw_at(sp + 8u);
+                *reinterpret_cast<u32u*>(a.out_base + dp + np - 4u) = dw_at(sp + np - 4u);
+            } else {
+                for (uint32_t b = 0; b < np; ++b) a.out_base[dp + b] = s_out[sp + b];
+            }
+        }
+#else
         for (uint32_t c = c0 + tid; !HPK_COMPACT_NOCOPY && c < ((D1 + 15u) >> 4); c += (uint32_t)G::kBlock) {
             const uint32_t x0 = max(c << 4, D0), x1 = min((c << 4) + 16u, D1);
             uint32_t i = s_map[c - c0], nxt = s_pre[i + 1], bi = s_iof[i] - s_pre[i];  // image byte of j: bi + j
@@ -957,6 +1002,7 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 for (uint32_t x = x0; x < x1; ++x) a.out_base[x] = (uint8_t)(w[(x & 15u) >> 2] >> (8 * (x & 3u)));
             }
         }
+#endif
     };
     // long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])

@@ -121,10 +121,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 // gathered into it (compact_fill), every listed literal takes its 4-rounded bound there when it is
 // listed (co_off). No device-wide cursor: one atomic per fill on one word would be ~290k per 32M-literal
 // launch, against the ~88 per us one word takes (MI355X_MICROARCH.md, dequeue).
-// a dword and four dwords stored at any byte address (unaligned global stores)
-typedef uint32_t u32u __attribute__((aligned(1)));
-typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-
 template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank, bool kCompact = false>
 __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     using G = GeoW<kWinB, kImgB>;
