@@ -821,30 +821,17 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
     };
     // kCompact: the decoded fill [fcur, fcur + fk) written back compacted (its kq queue entries give the
     // decoded literals' image offsets, written by literal into the window, free once the fill is
-    // decoded; nothing of it stays in registers, where it pushed the kernel into spills): a block scan of
-    // the lengths in literal order, ONE cursor add for the fill's total, then the destination written in
-    // whole 16-byte chunks: a map from each chunk to the literal holding its first byte (made by the
-    // literals' threads), a chunk inside one literal assembled from five image dwords by alignbyte, one
-    // that spans literals byte by byte; lengths, statuses and offsets. (Measured first: a binary search
-    // per chunk and byte reads, 2.47 ms per config-5 launch; per-literal dword copies by the literals'
-    // threads, 2.16 ms, ~840 us of it the copies, whose partial lines cost 1.13x the decoded bytes in
-    // HBM writes.) Listed literals (kListed) are 0 bytes here.
-#ifndef HPK_COMPACT_STATIC
-#define HPK_COMPACT_STATIC 0
-#endif
-#ifndef HPK_CF_LANE
-#define HPK_CF_LANE 1  // round 5: lane stores of whole literals instead of the chunk gather
-#endif
+    // decoded): a block scan of the lengths in literal order, ONE cursor add for the fill's total, then
+    // each thread stores its literals' bytes (round 5: unaligned 16-byte pieces, as the wave kernel's
+    // compact_fill; the round-4 per-chunk gather measured 97 us on config 2 against 90-91), lengths,
+    // statuses and offsets. Listed literals (kListed) are 0 bytes here.
 #ifndef HPK_COMPACT_NOCOPY
 #define HPK_COMPACT_NOCOPY 0  // (measurement only: no copy, no lengths)
 #endif
-    [[maybe_unused]] uint32_t wg_cur = BA < BB ? a.out_off[BA] : 0u;  // (HPK_COMPACT_STATIC only)
     auto compact_flush = [&](uint32_t fcur, uint32_t fk, uint32_t kqc) {
         lds_barrier();  // every length and status of the fill is in s_lenst; the window is free
-        uint32_t* const s_pre = reinterpret_cast<uint32_t*>(s_in);
-        uint32_t* const s_iof = s_pre + kQ + 1;
-        uint16_t* const s_map = reinterpret_cast<uint16_t*>(s_iof + kQ);
-        static_assert((2 * kQ + 1) * 4 + (kO / 16 + 2) * 2 <= kW, "compacted write-back tables in the window");
+        uint32_t* const s_iof = reinterpret_cast<uint32_t*>(s_in);  // [kQ] image offsets by literal
+        static_assert(kQ * 4 <= kW, "compacted write-back table in the window");
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // the image offsets, from the queue (still intact)
             const uint32_t q = tid + (uint32_t)G::kBlock * r;
@@ -879,45 +866,23 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
             carry += tot;
             lds_barrier();  // (s_hist again in the next round)
         }
-#if HPK_COMPACT_STATIC  // (measurement only: the workgroup's fills packed into its range's bound span, no cursor)
-        const uint32_t base = wg_cur;
-        wg_cur += carry;
-        lds_barrier();
-#else
         if (tid == 0) s_hist[32] = atomicAdd(a.cursor, carry);
         lds_barrier();
         const uint32_t base = s_hist[32];
-#endif
-        // the fill's prefix sums and a map from each destination chunk to the literal holding its first
-        // byte, over the window too
-        const uint32_t D0 = a.out_mis + base, D1 = D0 + carry, c0 = D0 >> 4;
+        const uint32_t D0 = a.out_mis + base;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t t = tid + (uint32_t)G::kBlock * r;
-            if (t < fk) {
-                s_pre[t] = exs[r];
-                const uint32_t ln = lenof(lst[r]);
-                const uint32_t d = D0 + exs[r], e = d + ln;
-                if (!HPK_CF_LANE && ln) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
-                    const uint32_t clo = d == D0 ? c0 : (d + 15u) >> 4;
-                    for (uint32_t c = clo; c <= ((e - 1u) >> 4); ++c) s_map[c - c0] = (uint16_t)t;
-                }
-                if (lst[r] != kListed && !HPK_COMPACT_NOCOPY) {
-                    a.co_off[fcur + t] = base + exs[r];
-                    a.out_len[fcur + t] = ln;
-                    a.status[fcur + t] = (uint8_t)(lst[r] >> 24);
-                }
+            if (t < fk && lst[r] != kListed && !HPK_COMPACT_NOCOPY) {
+                a.co_off[fcur + t] = base + exs[r];
+                a.out_len[fcur + t] = lenof(lst[r]);
+                a.status[fcur + t] = (uint8_t)(lst[r] >> 24);
             }
         }
-        if (tid == 0) s_pre[fk] = carry;
-        lds_barrier();
         const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_out);
-#if HPK_CF_LANE
         // (round 5, as the wave kernel's compact_fill) each thread stores literals tid and tid + kBlock
         // from the image in 16-byte pieces at any byte address, a literal's last piece ending at its
         // last byte; 4..15 bytes in dwords the same way, fewer bytewise
-        (void)D1;
-        (void)c0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t t = tid + (uint32_t)G::kBlock * r;
@@ -949,60 +914,6 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                 for (uint32_t b = 0; b < np; ++b) a.out_base[dp + b] = s_out[sp + b];
             }
         }
-#else
-        for (uint32_t c = c0 + tid; !HPK_COMPACT_NOCOPY && c < ((D1 + 15u) >> 4); c += (uint32_t)G::kBlock) {
-            const uint32_t x0 = max(c << 4, D0), x1 = min((c << 4) + 16u, D1);
-            uint32_t i = s_map[c - c0], nxt = s_pre[i + 1], bi = s_iof[i] - s_pre[i];  // image byte of j: bi + j
-            if (x0 == (c << 4) && x1 == (c << 4) + 16u && x1 - D0 <= nxt) {
-                // a whole chunk inside one literal: five image dwords, four alignbytes, one 16-byte store
-                const uint32_t sp = bi + (x0 - D0);
-                const uint32_t* q = img32 + (sp >> 2);
-                const uint32_t v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], sh = sp & 3u;
-                reinterpret_cast<uint4*>(a.out_base)[c] =
-                    make_uint4(__builtin_amdgcn_alignbyte(v1, v0, sh), __builtin_amdgcn_alignbyte(v2, v1, sh),
-                               __builtin_amdgcn_alignbyte(v3, v2, sh), __builtin_amdgcn_alignbyte(v4, v3, sh));
-                continue;
-            }
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            // the chunk's literals i .. i + 3 read at once (prefix sums b1..b4 past i's start), so its
-            // bytes' image reads are independent of each other; more than four (short or empty
-            // literals) step one by one
-            const uint32_t m1 = min(i + 1u, fk), m2 = min(i + 2u, fk), m3 = min(i + 3u, fk), m4 = min(i + 4u, fk);
-            const uint32_t b1 = s_pre[m1], b2 = s_pre[m2], b3 = s_pre[m3], b4 = s_pre[m4];
-            const uint32_t o1 = s_iof[min(m1, fk - 1u)] - b1, o2 = s_iof[min(m2, fk - 1u)] - b2;
-            const uint32_t o3 = s_iof[min(m3, fk - 1u)] - b3;
-            if (x1 - D0 <= b4 || m4 == fk) {
-#pragma unroll
-                for (int bb = 0; bb < 16; ++bb) {
-                    const uint32_t x = (c << 4) + (uint32_t)bb;
-                    if (x >= x0 && x < x1) {
-                        const uint32_t j = x - D0;
-                        const uint32_t src = j >= b3 ? o3 : j >= b2 ? o2 : j >= b1 ? o1 : bi;
-                        w[bb >> 2] |= (uint32_t)s_out[src + j] << (8 * (bb & 3));
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int bb = 0; bb < 16; ++bb) {
-                    const uint32_t x = (c << 4) + (uint32_t)bb;
-                    if (x >= x0 && x < x1) {
-                        const uint32_t j = x - D0;
-                        while (j >= nxt) {  // (empty literals between: equal prefix sums)
-                            ++i;
-                            nxt = s_pre[i + 1];
-                            bi = s_iof[i] - s_pre[i];
-                        }
-                        w[bb >> 2] |= (uint32_t)s_out[bi + j] << (8 * (bb & 3));
-                    }
-                }
-            }
-            if (x0 == (c << 4) && x1 == (c << 4) + 16u) {
-                reinterpret_cast<uint4*>(a.out_base)[c] = make_uint4(w[0], w[1], w[2], w[3]);
-            } else {
-                for (uint32_t x = x0; x < x1; ++x) a.out_base[x] = (uint8_t)(w[(x & 15u) >> 2] >> (8 * (x & 3u)));
-            }
-        }
-#endif
     };
     // long literals left to the long-literal phase are listed in a.long_list[BA, BB): those of
     // >= long_big encoded bytes from the front, the others from the back (counts in s_ctr[6], [7])

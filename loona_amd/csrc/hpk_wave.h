@@ -51,10 +51,6 @@
                         // (lit_acc_body, LUT4) instead of four bytes: measured 847-863 us against 804-821
                         // (round 5, profiles/r05/ab_acc_dword_*rejected.jsonl, software-pipelined or not)
 #endif
-#ifndef HPK_CW_LANE
-#define HPK_CW_LANE 1  // v33: the compacted form's write-back by lane (each lane its two literals) instead
-                       // of the chunk gather (compact_fill)
-#endif
 #ifndef HPK_CW_LANE_DIAG
 #define HPK_CW_LANE_DIAG 0  // (measurement only) 2: no copy loop, 3: 16-byte pieces at 16-aligned
                             // addresses, 4: no 16-byte stores
@@ -390,35 +386,26 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             }
             ri0 = ri1 = 0xFFFFFFFFu;
         };
-        // (kCompact) the decoded fill [fcur, fcur + fk) packed into the workgroup's span: its lengths in
-        // literal order (the window, dead once the fill is decoded, holds the tables), a wave scan, ONE
-        // LDS cursor add for the fill's total, offsets / lengths / statuses, then the destination in whole
-        // 16-byte chunks (the fill kernel's compact_flush, hpk_decode12.h): a map from each chunk to the
-        // literal holding its first byte, a chunk inside one literal made from five image dwords by
-        // alignbyte, one across literals byte by byte. q1 / q2: the lane's two queue entries (image offsets)
+        // (kCompact) the decoded fill [fcur, fcur + fk) packed into the workgroup's span (round 5, v33):
+        // its lengths by literal into the window (dead once the fill is decoded), a wave scan, ONE LDS
+        // cursor add for the fill's total; then each lane stores its own two slots' literals (the snake's
+        // long-with-short pair) from the image to their destinations in 16-byte stores at any byte address
+        // (the hardware's unaligned global accesses): a literal of n >= 16 bytes in pieces at 0, 16, ...
+        // and its last piece ending at n (rewriting some of its bytes with the same values), one of 4..15
+        // bytes in dwords the same way, a shorter one bytewise; each stored dword from two image dwords by
+        // alignbyte; the pair's pieces in one loop. Then offsets / lengths / statuses. (The per-chunk
+        // gather this replaced, a map from each 16-byte destination chunk to its literal and five image
+        // dwords of each of two literals per chunk, cost 1.37-1.45 ms per config-5 shard against
+        // 1.12-1.14: DESIGN §4.1d.) q1 / q2: the lane's two queue entries (image offsets)
         auto compact_fill = [&](uint32_t fcur, uint32_t fk, const uint2 q1, const uint2 q2) {
             uint32_t* const s_len = reinterpret_cast<uint32_t*>(s_win);  // [128] len | status << 24, kListed
-            uint32_t* const s_iof = s_len + 128;                          // [128] image offsets
-            // [133] per literal (its exclusive prefix sum p, the image offset of its byte j = so + j);
-            // entries 128..132 past the fill: (tot, 0)
-            uint2* const s_rec = reinterpret_cast<uint2*>(s_iof + 128);
-            uint16_t* const s_map = reinterpret_cast<uint16_t*>(s_rec + 134);
-            uint32_t* const s_rec_ex = reinterpret_cast<uint32_t*>(s_rec);  // (HPK_CW_LANE)
-            static_assert((128 + 128 + 2 * 134) * 4 + (G::kImg / 16 + 2) * 2 <= kWinB, "compact tables in the window");
+            uint32_t* const s_ex = s_len + 128;                           // [128] exclusive prefix sums
+            static_assert(256 * 4 <= kWinB, "compact tables in the window");
             s_len[lane] = kListed;
             s_len[lane + 64u] = kListed;
-            s_iof[lane] = 0u;
-            s_iof[lane + 64u] = 0u;
-            if (ri0 != 0xFFFFFFFFu) {
-                s_len[ri0] = rv0;
-                s_iof[ri0] = (q1.y >> 12) & 0x1FFFFu;
-            }
-            if (ri1 != 0xFFFFFFFFu) {
-                s_len[ri1] = rv1;
-                s_iof[ri1] = (q2.y >> 12) & 0x1FFFFu;
-            }
+            if (ri0 != 0xFFFFFFFFu) s_len[ri0] = rv0;
+            if (ri1 != 0xFFFFFFFFu) s_len[ri1] = rv1;
             const uint32_t l0 = s_len[lane], l1 = s_len[lane + 64u];
-            const uint32_t f0 = s_iof[lane], f1 = s_iof[lane + 64u];
             const uint32_t x0 = l0 == kListed ? 0u : l0 & 0xFFFFFFu, x1 = l1 == kListed ? 0u : l1 & 0xFFFFFFu;
             const uint32_t i0 = wave_incl_scan(x0, lane), i1 = wave_incl_scan(x1, lane);
             const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
@@ -427,41 +414,8 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             uint32_t u = 0;
             if (lane == 0) u = atomicAdd(&s_ctr[9], tot);
             const uint32_t base = wg0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)u);  // (blob-relative)
-            // offsets, lengths, statuses: stored last (a spill reload in between waits for every older
-            // vector-memory operation, these stores included)
-            auto results = [&]() {
-                if (lane < fk && l0 != kListed) {
-                    a.co_off[fcur + lane] = base + ex0;
-                    a.out_len[fcur + lane] = x0;
-                    a.status[fcur + lane] = (uint8_t)(l0 >> 24);
-                }
-                if (lane + 64u < fk && l1 != kListed) {
-                    a.co_off[fcur + lane + 64u] = base + ex1;
-                    a.out_len[fcur + lane + 64u] = x1;
-                    a.status[fcur + lane + 64u] = (uint8_t)(l1 >> 24);
-                }
-            };
-#ifndef HPK_CW_DIAG
-#define HPK_CW_DIAG 0  // (measurement only) 1: no map and no gather, 2: the map but no gather, 3: no byte path
-#endif
-            if (tot == 0u || HPK_CW_DIAG == 1) {
-                results();
-                return;
-            }
-            const uint32_t D0 = a.out_mis + base, D1 = D0 + tot, c0 = D0 >> 4;
-#if HPK_CW_LANE
-            // (v33) each lane copies its own two slots' literals (the snake's long-with-short pair) from
-            // the image to their destinations in 16-byte stores at any byte alignment (the hardware's
-            // unaligned global accesses): a literal of n >= 16 bytes in pieces at 0, 16, ... and its last
-            // piece ending at n (rewriting some of its bytes with the same values), one of 4..15 bytes in
-            // dwords the same way, a shorter one bytewise; each stored dword from two image dwords by
-            // alignbyte; the pair's pieces in one loop
-            (void)D1;
-            (void)c0;
-            (void)f0;
-            (void)f1;
-            {
-                uint32_t* const s_ex = s_rec_ex;  // [128] exclusive prefix by literal index
+            if (tot != 0u) {
+                const uint32_t D0 = a.out_mis + base;
                 s_ex[lane] = ex0;
                 s_ex[lane + 64u] = ex1;
                 __builtin_amdgcn_wave_barrier();
@@ -528,84 +482,18 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     }
                 }
             }
-            results();
-            return;
-#endif
-            s_rec[lane] = make_uint2(ex0, f0 - ex0);
-            s_rec[lane + 64u] = make_uint2(ex1, f1 - ex1);
-            if (lane < 6u) s_rec[128u + lane] = make_uint2(tot, 0u);  // (the chunk reads look ahead)
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {  // the chunks whose first byte (max(16 c, D0)) lies in [d, e)
-                const uint32_t t = lane + 64u * r, ln = r ? x1 : x0;
-                const uint32_t d = D0 + (r ? ex1 : ex0), e = d + ln;
-                if (ln) {
-                    const uint32_t clo = d == D0 ? c0 : (d + 15u) >> 4;
-                    for (uint32_t c = clo; c <= ((e - 1u) >> 4); ++c) s_map[c - c0] = (uint16_t)t;
-                }
+            // offsets, lengths, statuses: stored last (a spill reload in between waits for every older
+            // vector-memory operation, these stores included)
+            if (lane < fk && l0 != kListed) {
+                a.co_off[fcur + lane] = base + ex0;
+                a.out_len[fcur + lane] = x0;
+                a.status[fcur + lane] = (uint8_t)(l0 >> 24);
             }
-            if (HPK_CW_DIAG == 2) {
-                results();
-                return;
+            if (lane + 64u < fk && l1 != kListed) {
+                a.co_off[fcur + lane + 64u] = base + ex1;
+                a.out_len[fcur + lane + 64u] = x1;
+                a.status[fcur + lane + 64u] = (uint8_t)(l1 >> 24);
             }
-            const uint32_t* const img32 = reinterpret_cast<const uint32_t*>(s_img);
-            // (image addresses are clamped into the image: the reads below also address literals a chunk
-            // does not take)
-            for (uint32_t c = c0 + lane; c < ((D1 + 15u) >> 4); c += 64u) {
-                const uint32_t x0c = max(c << 4, D0), x1c = min((c << 4) + 16u, D1);
-                // the literal holding the chunk's first byte (i) and the next two: where they start
-                // (relative to D0) and their image offsets (byte j at so + j)
-                const uint32_t i = s_map[c - c0];
-                const uint2 ra = s_rec[i], rb = s_rec[i + 1], rc = s_rec[i + 2], rd = s_rec[i + 3];
-                // (read together: left to itself the compiler sank each read into the branch using it, one
-                // LDS round trip after another)
-                asm volatile("" ::"v"(ra.x), "v"(ra.y), "v"(rb.x), "v"(rb.y), "v"(rc.x), "v"(rd.x));
-                if (x0c == (c << 4) && x1c == (c << 4) + 16u) {
-                    // a whole chunk: five image dwords of literal i and five of literal i + 1 (the chunk's
-                    // bytes at their offsets), each output dword from one of them or merged across the
-                    // boundary; a chunk reaching a third literal (one of < 16 bytes) goes bytewise
-                    const uint32_t d0 = (c << 4) - D0;
-                    const uint32_t aa = min(ra.y + d0, (uint32_t)kImgB - 20u), ab = min(rb.y + d0, (uint32_t)kImgB - 20u);
-                    uint32_t A[5], B[5];
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) {
-                        A[j] = img32[(aa >> 2) + (uint32_t)j];
-                        B[j] = img32[(ab >> 2) + (uint32_t)j];
-                    }
-                    if (d0 + 16u <= rc.x || (rc.x == rd.x && d0 + 16u <= rd.x)) {
-                        // (an empty literal i + 2 with i + 3 past the chunk: the same two literals)
-                        const uint32_t pb = rb.x;  // where literal i + 1 starts
-                        uint32_t v[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const uint32_t d = d0 + 4u * (uint32_t)q;
-                            const uint32_t wa = __builtin_amdgcn_alignbyte(A[q + 1], A[q], aa & 3u);
-                            const uint32_t wb = __builtin_amdgcn_alignbyte(B[q + 1], B[q], ab & 3u);
-                            // bytes of wa: all below pb (none when d >= pb)
-                            const uint32_t m = d + 4u <= pb ? 0xFFFFFFFFu : d >= pb ? 0u : ~(0xFFFFFFFFu << (8u * (pb - d)));
-                            v[q] = (wa & m) | (wb & ~m);
-                        }
-                        if (pb == ra.x || pb == rc.x) {  // (an empty literal i or i + 1: bytewise, below)
-                        } else {
-                            reinterpret_cast<uint4*>(a.out_base)[c] = make_uint4(v[0], v[1], v[2], v[3]);
-                            continue;
-                        }
-                    }
-                }
-                // the fill's first and last chunk (partial), or one holding more literals: byte by byte
-                if (HPK_CW_DIAG == 3) continue;
-                uint32_t ii = i, bn = rb.x, ss = ra.y;
-                for (uint32_t x = x0c; x < x1c; ++x) {
-                    const uint32_t j = x - D0;
-                    while (j >= bn) {  // (empty and listed literals: equal prefix sums)
-                        ++ii;
-                        const uint2 r2 = s_rec[ii], r3 = s_rec[ii + 1];
-                        bn = r3.x;
-                        ss = r2.y;
-                    }
-                    a.out_base[x] = s_img[ss + j];
-                }
-            }
-            results();
         };
         while (cur < ce) {  // wave-uniform
             const uint32_t cntl = min(128u, ce - cur);
