@@ -236,10 +236,12 @@ def time_launches(codec, sets, stream, steps, warmup):
 
 
 def cuda_time(fn, reps, stream):
-    """Seconds per call of fn (device work on `stream`), HIP events around reps back-to-back calls."""
+    """Seconds per call of fn (device work on `stream`), HIP events around reps back-to-back calls after
+    three untimed ones (round 5: cold first launches read ~7 % slow, DESIGN §5 Timers)."""
     import torch
 
-    fn()
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
