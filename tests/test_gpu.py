@@ -1119,7 +1119,7 @@ def test_compact_unaligned_bases(codec, shift):
     """The compacted form on blobs whose bases are not 16-, 4- or 2-aligned (the wave kernel's lane
     stores are 16-byte pieces at any byte address, their last piece ending at the literal's last
     byte): literals of 0-3 decoded bytes (bytewise), 4-15 (dwords), 16-100 (pieces) and >= 64 encoded
-    bytes (listed for the long-literal phase), a literal with bad padding; bytes equal the oracle's,
+    bytes (listed for the long-literal phase), two of >= 8 KiB (the huge phase), bad padding; bytes equal the oracle's,
     literals disjoint, nothing written outside [0, out_off[n]) of the output (guard bytes)."""
     from hpk_util import oracle_encode
 
@@ -1134,6 +1134,8 @@ def test_compact_unaligned_bases(codec, shift):
         k = i % 10
         n = int(g.integers(0, 4)) if k == 0 else int(g.integers(4, 16)) if k < 4 else \
             int(g.integers(16, 101)) if k < 9 else int(g.integers(100, 400))
+        if i in (1234, 2345):  # two huge literals (>= 8 KiB encoded: the huge-literal phase)
+            n = 14000 + i
         s = bytes(alpha[g.integers(0, alpha.size, size=n)])
         if i % 97 == 5:
             s = bytes(g.integers(0, 256, size=n, dtype=np.uint8))
