@@ -9,7 +9,8 @@
 #              HPK_COMPACT=1 the compacted form, summaries named pmc_compact_*)
 #   lds        LDS bank-conflict attribution: SQ counters of libhpk_diag.so modes 0 8 9 10 on config 5
 #   trace      rocprofv3 --kernel-trace --stats of a short bench run
-#   bench      bench.py (reads the pmc summaries of this OUT when present)
+#   bench      bench.py (reads the pmc summaries of this OUT when present; BENCH_ARGS after, so
+#              BENCH_ARGS="--pmc-dir profiles" reads the committed ones)
 # Output under gpurun_out/$TAG.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -67,7 +68,7 @@ for l in open('$OUT/dec_time.jsonl'):
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu > $OUT/bench_trace.log 2>&1 || { echo "trace failed"; tail $OUT/bench_trace.log; exit 1; }
     tail -1 $OUT/bench_trace.log ;;
   bench)
-    timeout -k 10 600 python3 bench.py ${BENCH_ARGS} --pmc-dir $OUT > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }
+    timeout -k 10 600 python3 bench.py --pmc-dir $OUT ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }
     cat $OUT/bench.json ;;
   *) echo "unknown step $step"; exit 1 ;;
   esac
