@@ -530,7 +530,7 @@ def main():
                     w.drop_strings()
                     shards.append((w.enc_blob, w.enc_off))
 
-        def decode_fn(blob, off):  # the compacted form: the owner sends its written span as it is
+        def decode_fn(blob, off):  # the compacted form (its decoded bytes gathered end to end before they travel)
             return codec.decode_compact(blob, off, sync=False)
 
         res = shard.scatter_decode_gather(shards, decode_fn, device=dev, compacted=True)  # warm
@@ -549,9 +549,10 @@ def main():
             e2e = {"value": round(enc_total / dt / 2**30, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 3),
                    "steps": reps, "statuses_ok": bool(ok),
                    "what": "rank 0 holds the 8 shards; RCCL grouped send/recv of offsets + blob to each owner, "
-                           "device decode in the compacted form (hpk_decode_batch_compact: decoded bytes back to "
-                           "back, no gather pass), one all-reduce of the written sizes, RCCL send/recv of "
-                           "bytes/offsets/out_len/status back; no host copy of the data"}
+                           "device decode in the compacted form (hpk_decode_batch_compact), the decoded bytes "
+                           "gathered end to end on the owner (the wave kernel's span has gaps between "
+                           "workgroup shares), one all-reduce of the decoded sizes, RCCL send/recv of "
+                           "bytes/out_len/status back; no host copy of the data"}
         del res, shards
 
     line = None

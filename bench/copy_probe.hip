@@ -19,50 +19,70 @@
         }                                                                                     \
     } while (0)
 
-// kRd / kWr: read / write the two buffers; chunks are 16 B, nr / nw chunks in each
-template <bool kRd, bool kWr>
+// kRd / kWr: read / write the two buffers; chunks are 16 B, nr / nw chunks in each; kNt: nontemporal
+// stores (1), loads and stores (2); kF: chunks in flight per lane
+template <bool kRd, bool kWr, int kNt = 0, int kF = 4>
 __global__ __launch_bounds__(1024) void stream(const uint4* __restrict__ in, uint64_t nr, uint4* __restrict__ out,
                                                uint64_t nw, uint32_t* sink) {
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t acc = 0;
     const uint64_t n = nr > nw ? nr : nw;
-    for (uint64_t i = t0; i < n; i += 4 * T) {
-        uint4 v[4];
+    for (uint64_t i = t0; i < n; i += kF * T) {
+        uint4 v[kF];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kF; ++k) {
             const uint64_t j = i + k * T;
-            v[k] = kRd && j < nr ? in[j] : make_uint4((uint32_t)j, 1u, 2u, 3u);
+            if (kRd && j < nr) {
+                if (kNt >= 2) {
+                    v[k].x = __builtin_nontemporal_load(&in[j].x);
+                    v[k].y = __builtin_nontemporal_load(&in[j].y);
+                    v[k].z = __builtin_nontemporal_load(&in[j].z);
+                    v[k].w = __builtin_nontemporal_load(&in[j].w);
+                } else {
+                    v[k] = in[j];
+                }
+            } else {
+                v[k] = make_uint4((uint32_t)j, 1u, 2u, 3u);
+            }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kF; ++k) {
             const uint64_t j = i + k * T;
-            if (kWr && j < nw) out[j] = v[k];
+            if (kWr && j < nw) {
+                if (kNt >= 1) {
+                    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                    const v4u x = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(&out[j]));
+                }
+                else
+                    out[j] = v[k];
+            }
             acc += v[k].x ^ v[k].w;
         }
     }
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
-template <bool kRd, bool kWr>
+template <bool kRd, bool kWr, int kNt = 0, int kF = 4>
 static void run(const char* name, const uint4* in, uint64_t nr, uint4* out, uint64_t nw, uint32_t* sink, int blocks,
                 int threads) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((stream<kRd, kWr>), dim3(blocks), dim3(threads), 0, 0, in, nr, out, nw, sink);
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((stream<kRd, kWr, kNt, kF>), dim3(blocks), dim3(threads), 0, 0, in, nr, out, nw, sink);
     const int reps = 20;
     CK(hipEventRecord(a));
     for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL((stream<kRd, kWr>), dim3(blocks), dim3(threads), 0, 0, in, nr, out, nw, sink);
+        hipLaunchKernelGGL((stream<kRd, kWr, kNt, kF>), dim3(blocks), dim3(threads), 0, 0, in, nr, out, nw, sink);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
     const double us = ms * 1e3 / reps;
     const double bytes = (kRd ? nr * 16.0 : 0) + (kWr ? nw * 16.0 : 0);
-    printf("{\"variant\": \"%s\", \"blocks\": %d, \"threads\": %d, \"us\": %.1f, \"GB_s\": %.1f}\n", name, blocks, threads,
-           us, bytes / us * 1e-3);
+    printf("{\"variant\": \"%s\", \"nt\": %d, \"inflight\": %d, \"blocks\": %d, \"threads\": %d, \"us\": %.1f, \"GB_s\": %.1f}\n", name, kNt, kF,
+           blocks, threads, us, bytes / us * 1e-3);
 }
 
 int main() {
@@ -75,10 +95,20 @@ int main() {
     CK(hipMalloc(&sink, 4));
     CK(hipMemset(in, 1, nr * 16));
     for (int cfg = 0; cfg < 2; ++cfg) {
-        const int blocks = cfg ? 512 : 256, threads = cfg ? 1024 : 1024;
+        const int blocks = cfg ? 512 : 256, threads = 1024;
         run<true, false>("read", in, nr, out, nw, sink, blocks, threads);
         run<false, true>("write", in, nr, out, nw, sink, blocks, threads);
         run<true, true>("copy", in, nr, out, nw, sink, blocks, threads);
+        run<false, true, 1>("write", in, nr, out, nw, sink, blocks, threads);
+        run<true, true, 1>("copy", in, nr, out, nw, sink, blocks, threads);
+        run<true, true, 2>("copy", in, nr, out, nw, sink, blocks, threads);
+        run<true, true, 0, 8>("copy", in, nr, out, nw, sink, blocks, threads);
+        run<true, true, 1, 8>("copy", in, nr, out, nw, sink, blocks, threads);
+        run<true, false, 0, 8>("read", in, nr, out, nw, sink, blocks, threads);
     }
+    // the float4 copy of the microarchitecture guide: one 16-byte chunk per thread, a grid over the buffer
+    run<true, true, 0, 1>("copy_flat", in, nr, out, nr, sink, (int)((nr + 1023) / 1024), 1024);
+    run<true, true, 1, 1>("copy_flat", in, nr, out, nr, sink, (int)((nr + 1023) / 1024), 1024);
+    run<true, true, 0, 1>("copy_flat256", in, nr, out, nr, sink, (int)((nr + 255) / 256), 256);
     return 0;
 }

@@ -117,8 +117,10 @@ int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
 
 /* ---- batch decode, compacted output --------------------------------------
  * The reference returns each literal as an exact-length Vec (huffman.rs:98, 160); this form writes
- * the decoded bytes back to back instead of into bound-sized regions: on return literal i's bytes are
- * out_blob[out_off[i] .. out_off[i] + out_len[i]) and out_off[n] is the end of everything written.
+ * each literal's decoded bytes exactly, in runs with no region slack between a run's literals, instead of
+ * into bound-sized regions: on return literal i's bytes are out_blob[out_off[i] .. out_off[i] + out_len[i])
+ * and out_off[n] is the end of the span written to. The span is NOT gap-free: see the layouts below
+ * (listed literals keep their bound, and the wave-fill kernel's workgroup shares end in unwritten tails).
  * out_off (n+1 entries) is an OUTPUT here. Literals are packed in runs (a fill of the kernel at a
  * time, literal order inside a run, runs in completion order), so out_off is not monotone. A literal
  * the kernel hands to its long- or huge-literal phase keeps a region of its 4-rounded decoded bound,

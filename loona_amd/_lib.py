@@ -229,10 +229,13 @@ def lib() -> ctypes.CDLL:
         L.hpk_henc_out_free.restype = None
         L.hpk_ctx_set_decode_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.hpk_ctx_set_decode_kernel.restype = ctypes.c_int
-        L.hpk_test_fail_batches.argtypes = [ctypes.c_int]
-        L.hpk_test_fail_batches.restype = None
-        L.hpk_test_bound_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
-        L.hpk_test_bound_scan.restype = ctypes.c_int
+        # test-only entry points: bound when the library has them (an A/B build of another source may not)
+        if hasattr(L, "hpk_test_fail_batches"):
+            L.hpk_test_fail_batches.argtypes = [ctypes.c_int]
+            L.hpk_test_fail_batches.restype = None
+        if hasattr(L, "hpk_test_bound_scan"):
+            L.hpk_test_bound_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+            L.hpk_test_bound_scan.restype = ctypes.c_int
         L.hpk_version.argtypes = []
         L.hpk_version.restype = ctypes.c_char_p
         _lib = L

@@ -272,10 +272,13 @@ class HuffmanCodec:
         return out_blob, out_off, out_len, status
 
     def decode_compact(self, in_blob, in_off, out_blob=None, out_off=None, out_len=None, status=None, sync=False):
-        """hpk_decode_batch_compact: torch cuda tensors -> (out_blob, out_off, out_len, status) with the
-        decoded bytes back to back (the reference's exact-length outputs, huffman.rs:98, 160): literal i
-        is out_blob[out_off[i] : out_off[i] + out_len[i]] and out_off[n] is the end of what was written.
-        out_off is an output (n + 1 entries; runs of literals in completion order, so not monotone)."""
+        """hpk_decode_batch_compact: torch cuda tensors -> (out_blob, out_off, out_len, status) with each
+        literal's decoded bytes written exactly (the reference's exact-length outputs, huffman.rs:98, 160):
+        literal i is out_blob[out_off[i] : out_off[i] + out_len[i]] and out_off[n] is the end of the span
+        written to. out_off is an output (n + 1 entries; runs of literals in completion order, so not
+        monotone). The span is not gap-free: listed (long / huge) literals keep their decoded bound, and
+        the wave-fill kernel (>= 4M literals) packs per workgroup, each share ending in an unwritten tail
+        (include/hpk.h); shard.compact gathers the bytes end to end."""
         import torch
 
         n = int(in_off.shape[0]) - 1

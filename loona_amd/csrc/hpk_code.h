@@ -86,24 +86,12 @@ static const uint8_t HPK_CODE_LEN[HPK_NSYM] = {
 #define HPK_L3_LEN0(e) (((e) >> 26) & 15u)
 #define HPK_L3_NOTTWO 0x80000000u
 
-// LUT4 (decode v31, the wave kernel's fills): the same codes in the layout of the dword-output step
-// (lit_or_body / lit_or_step), whose decoded bytes are OR-ed into a zeroed LDS image a dword at a time:
-//   [7:0] sym0 (0 without a code)  [15:8] sym1 (0 without a second code)  [20:16] bits held
-//   [23:21] len0 - 5 (0 without a code)  [31:24] 8 x codes held (0, 8, 16)
-// so an entry's bytes are its low half as they stand (zero above the codes it holds), the shift that
-// places the second entry's bytes after the first's is its top byte, and the output position advances
-// by the top bytes in units of bits. The shifts that take "bits held" use its low five bits only.
-#define HPK_L4_HELD(e) (((e) >> 16) & 31u)
-#define HPK_L4_LEN0(e) ((((e) >> 21) & 7u) + 5u)
-#define HPK_L4_C8(e) ((e) >> 24)
-
 struct hpk_tables {
     uint32_t code[HPK_NSYM];   // right-aligned canonical code
     uint8_t len[HPK_NSYM];     // code length in bits
     uint32_t lut[HPK_LUT_SIZE];
     uint32_t lut2[HPK_LUT_SIZE];
     uint32_t lut3[HPK_LUT_SIZE];
-    uint32_t lut4[HPK_LUT_SIZE];
     uint16_t lo[HPK_LO_SIZE];
     uint8_t t8[256];  // symbol of the <=8-bit code that prefixes each 8-bit window (0 past LIM8)
 };
@@ -193,8 +181,6 @@ static inline int hpk_build_tables(hpk_tables* t) {
         const uint32_t e2 = t->lut2[v], codes = HPK_L2_CODES(e2);
         t->lut3[v] = (e2 & 0xFFu) | (HPK_L2_HELD(e2) << 8) | (e2 & 0x00FF0000u) | (codes << 24) |
                      ((codes ? HPK_L2_LEN0(e2) : 15u) << 26) | (codes < 2 ? HPK_L3_NOTTWO : 0u);
-        t->lut4[v] = (codes ? (e2 & 0xFFu) : 0u) | (codes == 2 ? ((e2 >> 16) & 0xFFu) << 8 : 0u) |
-                     (HPK_L2_HELD(e2) << 16) | (codes ? (HPK_L2_LEN0(e2) - 5u) << 21 : 0u) | ((8u * codes) << 24);
     }
     return 0;
 }

@@ -59,9 +59,6 @@ extern "C" hpk_ctx* hpk_ctx_create(int device) {
     if ((e = hipMalloc(&c->d_lut3, sizeof(t->lut3))) != hipSuccess) return fail("hipMalloc lut3", e);
     if ((e = hipMemcpy(c->d_lut3, t->lut3, sizeof(t->lut3), hipMemcpyHostToDevice)) != hipSuccess)
         return fail("upload lut3", e);
-    if ((e = hipMalloc(&c->d_lut4, sizeof(t->lut4))) != hipSuccess) return fail("hipMalloc lut4", e);
-    if ((e = hipMemcpy(c->d_lut4, t->lut4, sizeof(t->lut4), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail("upload lut4", e);
     if ((e = hipMalloc(&c->d_lo, sizeof(t->lo))) != hipSuccess) return fail("hipMalloc lo", e);
     if ((e = hipMalloc(&c->d_t8, sizeof(t->t8))) != hipSuccess) return fail("hipMalloc t8", e);
     if ((e = hipMemcpy(c->d_t8, t->t8, sizeof(t->t8), hipMemcpyHostToDevice)) != hipSuccess) return fail("upload t8", e);
@@ -98,9 +95,12 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
             // destroyed by the caller: ADVICE r3.) Launches on a stream the context does not own always
             // record their slot's event (hpk_long_list_used), so the only slots without one were used on
             // the context's own stream: waiting for that stream drains them.
+            // Only those slots' (absent) events are cleared: a slot used on another stream keeps its
+            // recorded event, which the own-stream wait does not cover.
             c->long_multi = true;
             HIP_TRY(hipStreamSynchronize(c->own));
-            for (int k = 0; k < hpk_ctx::kLongSlots; ++k) c->long_ev_set[k] = false;
+            for (int k = 0; k < hpk_ctx::kLongSlots; ++k)
+                if (c->long_stream[k] == c->own) c->long_ev_set[k] = false;
         }
         j = 0;
         while (j < hpk_ctx::kLongSlots && c->long_list[j]) ++j;
@@ -129,8 +129,9 @@ int hpk_long_list(hpk_ctx* c, uint32_t n, uint32_t** list, int* slot) {
 int hpk_slot_drain(hpk_ctx* c, int j) {
     if (c->long_ev_set[j])
         HIP_TRY(hipEventSynchronize(c->long_ev[j]));
-    else if (c->long_list[j])  // single-stream mode on the own stream (foreign streams set events)
-        HIP_TRY(hipStreamSynchronize(c->stream));
+    else if (c->long_list[j])  // a slot without an event was last used on the own stream (foreign
+                               // streams always record theirs): wait for that stream, not the caller's
+        HIP_TRY(hipStreamSynchronize(c->own));
     return HPK_E_OK;
 }
 
@@ -151,7 +152,6 @@ extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     (void)hipFree(c->d_lut);
     (void)hipFree(c->d_lut2);
     (void)hipFree(c->d_lut3);
-    (void)hipFree(c->d_lut4);
     (void)hipFree(c->d_lo);
     (void)hipFree(c->d_t8);
     (void)hipFree(c->d_codes);

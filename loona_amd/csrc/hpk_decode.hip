@@ -246,7 +246,6 @@ static void decode_args(hpk_ctx* c, const hpk_batch& b, DecodeArgs& a) {
     a.lut = c->d_lut;
     a.lut2 = c->d_lut2;
     a.lut3 = c->d_lut3;
-    a.lut4 = c->d_lut4;
     a.dbg = nullptr;
     a.in_cap = b.in_cap;
     a.out_cap = b.out_cap;

@@ -78,12 +78,6 @@ __device__ __forceinline__ uint32_t win_at(const uint32_t* __restrict__ win32, u
 template <int kTab = 2>  // the table layout: 2 = LUT2, 3 = LUT3 (hpk_code.h)
 __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, bool& ok2) {
     // a length field the entry does not hold is 15, past any clamped rem (and t1 >= l1: ok2 => ok1)
-    if (kTab == 4) {  // LUT4: 8 x codes held in [31:24], len0 - 5 in [23:21], bits held in [20:16]
-        const uint32_t c8 = HPK_L4_C8(e), t1 = HPK_L4_HELD(e), l1 = HPK_L4_LEN0(e);
-        ok1 = (c8 != 0u) & (l1 <= rem);
-        ok2 = (c8 == 16u) & (t1 <= rem);
-        return ok2 ? t1 : (ok1 ? l1 : 0u);
-    }
     const uint32_t rc = min(rem, HPK_LUT2_CLAMP);
     if (kTab == 3) {
         const uint32_t l1 = HPK_L3_LEN0(e), t1 = HPK_L3_HELD(e);
@@ -98,12 +92,12 @@ __device__ __forceinline__ uint32_t lut12(uint32_t e, uint32_t rem, bool& ok1, b
 }
 template <int kTab>
 __device__ __forceinline__ bool lut_nottwo(uint32_t e) {
-    return kTab == 4 ? HPK_L4_C8(e) != 16u : kTab == 3 ? e >= HPK_L3_NOTTWO : e >= HPK_LUT2_NOTTWO;
+    return kTab == 3 ? e >= HPK_L3_NOTTWO : e >= HPK_LUT2_NOTTWO;
 }
-// An entry's second symbol byte, in place for a byte store (LUT2 / LUT3: [23:16], LUT4: [15:8])
+// An entry's second symbol byte, in place for a byte store (LUT2 / LUT3: [23:16])
 template <int kTab>
 __device__ __forceinline__ uint32_t lut_sym1(uint32_t e) {
-    return kTab == 4 ? e >> 8 : e >> 16;
+    return e >> 16;
 }
 
 // The decoded bytes of an entry, packed little-endian and zero above the g = ok1 + ok2 of them.
@@ -135,8 +129,6 @@ struct Lit12 {
     bool more;            // (kMore steps) the walk may go on: the last step used both entries whole, or
                           // decoded a long code; false once a step has proved that no code fits
     bool act;             // holds a fast-path literal not yet finalised
-    uint32_t pe1, pe2;    // (lit_or_body) the last body step's two entries, stored by the next step
-    uint32_t acc;         // (lit_acc_body) the pending dword's bytes below the output position
 };
 
 // (Re)load the pair and the next dword at X.
@@ -262,21 +254,6 @@ __device__ __forceinline__ void lit12_step(Lit12& L, const uint32_t* __restrict_
     if (lit12_step_main<kStore, kP1, kTab, kMore>(L, win32, lut, out8, dmy)) lit12_park<kStore, kMore>(L, win32, lo, out8);
 }
 
-// The tails of a lane's two literals (HPK_TAIL2, off: measured slower): both checked steps in one block, each doing nothing
-// once its literal's walk has ended (more = false), so the two independent lookup chains share their
-// waits; the leading-ones lookups after both. Semantics are lit12_step's.
-template <int kStore, bool kP1, int kTab>
-__device__ __forceinline__ void lit12_step2(Lit12& L, Lit12& N, const uint32_t* __restrict__ win32,
-                                            const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo,
-                                            uint8_t* __restrict__ out8, uint32_t dmy) {
-    const bool pL = lit12_step_main<kStore, kP1, kTab, true>(L, win32, lut, out8, dmy, L.more);
-    const bool pN = lit12_step_main<kStore, kP1, kTab, true>(N, win32, lut, out8, dmy, N.more);
-    if (pL | pN) {
-        if (pL) lit12_park<kStore, true>(L, win32, lo, out8);
-        if (pN) lit12_park<kStore, true>(N, win32, lo, out8);
-    }
-}
-
 // Body step (decode v27): the same two lookups with NO fit tests, for a literal with at least
 // kBodyMin bits left before the step. A step consumes <= 24 bits, so every code the two entries hold
 // ends inside the literal, and >= 13 bits are left after it. The stores are unconditional at the
@@ -313,15 +290,15 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
     if (kDup == 2) asm volatile("" ::"v"(((const volatile HPK_LDS_AS uint32_t*)win32)[(L.X >> 5) + 2]));
     const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
     const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
-    const uint32_t u1 = kTab == 4 ? HPK_L4_HELD(e1) : kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
+    const uint32_t u1 = kTab == 3 ? HPK_L3_HELD(e1) : HPK_L2_HELD(e1);
     const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
     if (kDup == 1) {
         const volatile HPK_LDS_AS uint32_t* vl = (const volatile HPK_LDS_AS uint32_t*)lut;
         asm volatile("" ::"v"(vl[w >> (32 - HPK_LUT_BITS)]));
         asm volatile("" ::"v"(vl[(w << u1) >> (32 - HPK_LUT_BITS)]));
     }
-    const uint32_t u2 = kTab == 4 ? HPK_L4_HELD(e2) : kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
-    const uint32_t o1 = L.o + (kTab == 4 ? HPK_L4_C8(e1) >> 3 : kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1));
+    const uint32_t u2 = kTab == 3 ? HPK_L3_HELD(e2) : HPK_L2_HELD(e2);
+    const uint32_t o1 = L.o + (kTab == 3 ? HPK_L3_CODES(e1) : HPK_L2_CODES(e1));
     if (kStore != kNoStore) {
         if (kDup == 3) {
             volatile HPK_LDS_AS uint8_t* v8 = (volatile HPK_LDS_AS uint8_t*)out8;
@@ -335,7 +312,7 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
         out8[o1] = (uint8_t)e2;
         (out8 + 1)[o1] = (uint8_t)lut_sym1<kTab>(e2);
     }
-    L.o = o1 + (kTab == 4 ? HPK_L4_C8(e2) >> 3 : kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2));
+    L.o = o1 + (kTab == 3 ? HPK_L3_CODES(e2) : HPK_L2_CODES(e2));
     const uint32_t xn = L.X + u1 + u2;
     const bool cross = (xn ^ L.X) > 31u;
     L.d0 = cross ? L.d1 : L.d0;
@@ -369,293 +346,10 @@ __device__ __forceinline__ void lit12_body(Lit12& L, const uint32_t* __restrict_
     body = L.Eb - L.X >= kBodyMin;
 }
 
-// Two literals' body steps in one block (decode v32, the wave kernel): a lane's two literals L and N
-// step together, each while its body flag holds; a chain whose body has ended stands still (no advance)
-// and stores to the lane's dummy slot. One wave's instructions issue in order, so a step alone waits out
-// its two dependent table reads (~150 cycles each with the bank conflicts of 64 random addresses;
-// bench/step_probe.hip: the bare chain 398 cycles per step, the product step 638, one wave on an idle
-// CU); two independent chains in one block fill each other's waits. The byte stores and the long-code
-// branch are lit12_body's, chain by chain; semantics are lit12_body's (huffman.rs:95-161).
-template <int kStore, int kTab = 2>
-__device__ __forceinline__ void lit12_body2(Lit12& L, Lit12& N, const uint32_t* __restrict__ win32,
-                                            const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo,
-                                            uint8_t* __restrict__ out8, uint32_t dmy, bool& bl, bool& bn) {
-    auto held = [](uint32_t e) { return kTab == 3 ? HPK_L3_HELD(e) : HPK_L2_HELD(e); };
-    auto codes = [](uint32_t e) { return kTab == 3 ? HPK_L3_CODES(e) : HPK_L2_CODES(e); };
-    const uint32_t dL = win32[(L.X >> 5) + 2], dN = win32[(N.X >> 5) + 2];
-    const uint32_t wL = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X), wN = __builtin_amdgcn_alignbit(N.d0, N.d1, ~N.X);
-    const uint32_t eL1 = lut[wL >> (32 - HPK_LUT_BITS)], eN1 = lut[wN >> (32 - HPK_LUT_BITS)];
-    const uint32_t uL1 = held(eL1), uN1 = held(eN1);
-    const uint32_t eL2 = lut[(wL << uL1) >> (32 - HPK_LUT_BITS)], eN2 = lut[(wN << uN1) >> (32 - HPK_LUT_BITS)];
-    const uint32_t uL2 = held(eL2), uN2 = held(eN2);
-    // stores (an ended chain's to the dummy slot: its bytes past the output position may lie past its
-    // region), then the advance (none for an ended chain)
-    const uint32_t oL1 = L.o + codes(eL1), oN1 = N.o + codes(eN1);
-    if (kStore != kNoStore) {
-        const uint32_t aL = bl ? L.o : dmy, aL1 = bl ? oL1 : dmy, aN = bn ? N.o : dmy, aN1 = bn ? oN1 : dmy;
-        out8[aL] = (uint8_t)eL1;
-        (out8 + 1)[aL] = (uint8_t)(eL1 >> 16);
-        out8[aL1] = (uint8_t)eL2;
-        (out8 + 1)[aL1] = (uint8_t)(eL2 >> 16);
-        out8[aN] = (uint8_t)eN1;
-        (out8 + 1)[aN] = (uint8_t)(eN1 >> 16);
-        out8[aN1] = (uint8_t)eN2;
-        (out8 + 1)[aN1] = (uint8_t)(eN2 >> 16);
-    }
-    L.o = bl ? oL1 + codes(eL2) : L.o;
-    N.o = bn ? oN1 + codes(eN2) : N.o;
-    const uint32_t xL = L.X + (bl ? uL1 + uL2 : 0u), xN = N.X + (bn ? uN1 + uN2 : 0u);
-    const bool cL = (xL ^ L.X) > 31u, cN = (xN ^ N.X) > 31u;
-    L.d0 = cL ? L.d1 : L.d0;
-    L.d1 = cL ? L.d2 : L.d1;
-    L.d2 = cL ? dL : L.d2;
-    N.d0 = cN ? N.d1 : N.d0;
-    N.d1 = cN ? N.d2 : N.d1;
-    N.d2 = cN ? dN : N.d2;
-    L.X = xL;
-    N.X = xN;
-    const bool pL = bl & (uL2 == 0u), pN = bn & (uN2 == 0u);
-    if (pL | pN) {  // a 13..30-bit code or EOS (lit12_body's leading-ones branch), chain by chain
-        auto park = [&](Lit12& T) {
-            const uint32_t wp = __builtin_amdgcn_alignbit(T.d0, T.d1, ~T.X);
-            uint32_t sy, len;
-            bool eos;
-            lo_decode(wp, lo, sy, len, eos);
-            const uint32_t r = T.Eb - T.X;
-            if (len > r) {  // huffman.rs:128-134
-                T.st = HPK_PADDING_TOO_LARGE;
-                T.Eb = T.X;
-            } else if (eos) {  // huffman.rs:112-116
-                T.st = HPK_EOS_IN_STRING;
-                T.Eb = T.X;
-            } else {
-                if (kStore != kNoStore) out8[T.o] = (uint8_t)sy;
-                T.o += 1;
-                T.X += len;
-                lit12_load(T, win32);
-            }
-        };
-        if (pL) park(L);
-        if (pN) park(N);
-    }
-    bl = bl & (L.Eb - L.X >= kBodyMin);
-    bn = bn & (N.Eb - N.X >= kBodyMin);
-}
-
 // Final status of a literal whose walk has stopped; a status set by the walk wins.
 __device__ __forceinline__ uint32_t lit12_status(const Lit12& L) {
     if (L.st != HPK_OK) return L.st;
     return residual_status(L.Eb - L.X, __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X));
-}
-
-// ------------------------------------------------------------------------------------------
-// Dword output (decode v31, the wave kernel's fills). The literal is decoded into a ZEROED LDS image
-// by atomic ORs of whole dwords: a step's decoded bytes (up to four, zero above them) are shifted to
-// the output position's byte lane and OR-ed into the dword there and the next one (ds_or_b32, no
-// return). Two LDS stores per step replace four byte stores, and the dwords two literals share at
-// their edges need no order between the lanes that write them: an OR of zero bytes changes nothing.
-// L.o holds the output position in BITS (8 x the LDS byte address): the LUT4 entries' top bytes
-// advance it, and its low five bits are the shift that places a step's bytes. Semantics are
-// lit12_body's / lit12_step's (huffman.rs:95-161); only the stores differ.
-#ifndef HPK_SCHED_FENCE
-#define HPK_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
-__device__ __forceinline__ void or_dword(uint32_t* __restrict__ img32, uint32_t d, uint32_t v) {
-    __hip_atomic_fetch_or(&img32[d], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void or_out(uint32_t* __restrict__ img32, uint32_t o8, uint32_t v) {
-    const uint64_t t = (uint64_t)v << (o8 & 24u);
-    or_dword(img32, o8 >> 5, (uint32_t)t);
-    or_dword(img32, (o8 >> 5) + 1u, (uint32_t)(t >> 32));
-}
-
-// The leading-ones branch of both steps: a 13..30-bit code or EOS at X with > 12 bits left.
-__device__ __forceinline__ void lit_or_long(Lit12& L, const uint32_t* __restrict__ win32, const uint16_t* __restrict__ lo,
-                                            uint32_t* __restrict__ img32) {
-    const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-    uint32_t sy, len;
-    bool eos;
-    lo_decode(wp, lo, sy, len, eos);
-    const uint32_t r = L.Eb - L.X;
-    if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
-        L.st = HPK_PADDING_TOO_LARGE;
-        L.Eb = L.X;
-        L.more = false;
-    } else if (eos) {  // huffman.rs:112-116
-        L.st = HPK_EOS_IN_STRING;
-        L.Eb = L.X;
-        L.more = false;
-    } else {
-        or_dword(img32, L.o >> 5, sy << (L.o & 24u));  // (one byte: never crosses a dword)
-        L.o += 8u;
-        L.X += len;
-        lit12_load(L, win32);
-    }
-}
-
-// The bytes of a body step's two entries (pe1, pe2), OR-ed at L.o, which then moves past them.
-__device__ __forceinline__ void lit_or_pend(Lit12& L, uint32_t* __restrict__ img32) {
-    or_out(img32, L.o, (L.pe1 & 0xFFFFu) | ((L.pe2 & 0xFFFFu) << HPK_L4_C8(L.pe1)));
-    L.o += HPK_L4_C8(L.pe1) + HPK_L4_C8(L.pe2);
-    L.pe1 = L.pe2 = 0u;
-}
-
-// Body step: lit12_body's two unchecked lookups (>= kBodyMin bits left), bytes OR-ed as a dword pair.
-// Software-pipelined: a step's entries are kept (pe1, pe2) and stored by the NEXT step while its first
-// lookup is in flight, so the walk's dependency chain (bit position -> window -> lookup -> lookup ->
-// bit position) carries no store work; lit_or_pend stores the last step's at the body's end.
-__device__ __forceinline__ void lit_or_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
-                                            const uint16_t* __restrict__ lo, uint32_t* __restrict__ img32, bool& body) {
-    const uint32_t d3 = win32[(L.X >> 5) + 2];
-    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
-    HPK_SCHED_FENCE();
-    lit_or_pend(L, img32);  // the previous step's bytes, under this step's first lookup
-    HPK_SCHED_FENCE();
-    const uint32_t e2 = lut[(w << ((e1 >> 16) & 31u)) >> (32 - HPK_LUT_BITS)];
-    const uint32_t u2 = HPK_L4_HELD(e2);
-    const uint32_t xn = L.X + HPK_L4_HELD(e1) + u2;
-    const bool cross = (xn ^ L.X) > 31u;
-    L.d0 = cross ? L.d1 : L.d0;
-    L.d1 = cross ? L.d2 : L.d1;
-    L.d2 = cross ? d3 : L.d2;
-    L.X = xn;
-    L.pe1 = e1;
-    L.pe2 = e2;
-    if (u2 == 0u) {  // e2 holds no code (nor e1, if it held none): its bytes first, then the long code's
-        lit_or_pend(L, img32);
-        lit_or_long(L, win32, lo, img32);
-    }
-    body = L.Eb - L.X >= kBodyMin;
-}
-
-// Checked step (the tails): lit12_step<.., kMore>'s fit tests, from LUT4's fields.
-__device__ __forceinline__ void lit_or_step(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
-                                            const uint16_t* __restrict__ lo, uint32_t* __restrict__ img32) {
-    const uint32_t d3 = win32[(L.X >> 5) + 2];
-    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-    const uint32_t rem = L.Eb - L.X;
-    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
-    const uint32_t c1 = HPK_L4_C8(e1), h1 = HPK_L4_HELD(e1), l1 = HPK_L4_LEN0(e1);
-    const bool a1 = (c1 != 0u) & (l1 <= rem);
-    const bool a2 = (c1 == 16u) & (h1 <= rem);
-    const uint32_t u1 = a2 ? h1 : (a1 ? l1 : 0u);
-    // a code longer than 12 bits (or EOS) starts here and may still fit (with more than 12 bits left,
-    // any code the entry holds fits: no first code <=> the entry has none)
-    bool park = !a1 & (rem > (uint32_t)HPK_LUT_BITS);
-    const bool cont = a1 & (a2 | (c1 != 16u));  // the first entry was consumed whole
-    const uint32_t rem2 = rem - u1;
-    const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
-    const uint32_t c2 = HPK_L4_C8(e2), h2 = HPK_L4_HELD(e2), l2 = HPK_L4_LEN0(e2);
-    const bool b1 = cont & (c2 != 0u) & (l2 <= rem2);
-    const bool b2 = cont & (c2 == 16u) & (h2 <= rem2);
-    park |= cont & !b1 & (rem2 > (uint32_t)HPK_LUT_BITS);
-    // both entries used whole: more codes may follow (otherwise the walk has ended, huffman.rs:100-123)
-    const bool more2 = b1 & (b2 | (c2 != 16u));
-    const uint32_t g1 = 8u * ((uint32_t)a1 + (uint32_t)a2), g2 = 8u * ((uint32_t)b1 + (uint32_t)b2);
-    const uint32_t v = __builtin_amdgcn_ubfe(e1, 0, g1) | (__builtin_amdgcn_ubfe(e2, 0, g2) << g1);
-    or_out(img32, L.o, v);
-    L.o += g1 + g2;
-    const uint32_t xn = L.X + u1 + (b2 ? h2 : (b1 ? l2 : 0u));
-    const bool cross = (xn ^ L.X) > 31u;
-    L.d0 = cross ? L.d1 : L.d0;
-    L.d1 = cross ? L.d2 : L.d1;
-    L.d2 = cross ? d3 : L.d2;
-    L.X = xn;
-    L.prog = a1 | park;
-    L.more = park | more2;
-    if (park) lit_or_long(L, win32, lo, img32);
-}
-
-// ------------------------------------------------------------------------------------------
-// Accumulated dword output (decode v32, the wave kernel's body steps in fills whose output regions
-// all start and end on 4-byte boundaries, as hpk_decoded_bound rounded up to 4 makes them). A step's
-// decoded bytes (up to four, LUT4: zero above the codes an entry holds) are shifted into the lane's
-// pending dword (L.pe1: the bytes of the dword holding the output position, zero from it on); the dword
-// is stored, whole and aligned, by the step that completes it, and every other step stores it to the
-// lane's dummy slot (no exec-mask branch). One ds_write_b32 per step replaces four ds_write_b8: the
-// byte stores were ~45 % of the body's LDS bank-conflict cycles (profiles/r04/lds_attribution/), and a
-// dword store to a random address costs what a byte store does. L.o is the output position in BITS
-// (8 x the LDS byte address) while the body runs. A dword the step completes lies inside the literal's
-// region: it ends at or before the output position, which stays below the region's end. acc_flush
-// stores the part-filled dword at the body's end, before the checked tail steps store bytes over its
-// upper part; the dword lies inside the region because the region's end is 4-aligned and above the
-// output position (>= 5 bits are left after a body step, so the decoded length stays below the
-// decoded bound). Semantics are lit12_body's (huffman.rs:95-161); only the stores differ.
-#ifndef HPK_ACC_PIPE
-#define HPK_ACC_PIPE 1
-#endif
-__device__ __forceinline__ void acc_put(Lit12& L, uint32_t v, uint32_t c8, uint8_t* __restrict__ out8, uint32_t dmy) {
-    const uint64_t t = (uint64_t)v << (L.o & 24u);
-    const uint32_t lo = L.acc | (uint32_t)t;
-    const uint32_t on = L.o + c8;
-    const bool full = (on ^ L.o) > 31u;  // (c8 <= 32: the dword at L.o is complete)
-    *reinterpret_cast<uint32_t*>(out8 + (full ? (L.o >> 3) & ~3u : dmy)) = lo;
-    L.acc = full ? (uint32_t)(t >> 32) : lo;
-    L.o = on;
-}
-// (HPK_ACC_PIPE) the bytes of the previous body step's entries (pe1, pe2; zero entries: nothing)
-__device__ __forceinline__ void acc_pend(Lit12& L, uint8_t* __restrict__ out8, uint32_t dmy) {
-    acc_put(L, (L.pe1 & 0xFFFFu) | ((L.pe2 & 0xFFFFu) << HPK_L4_C8(L.pe1)), HPK_L4_C8(L.pe1) + HPK_L4_C8(L.pe2), out8, dmy);
-    L.pe1 = L.pe2 = 0u;
-}
-__device__ __forceinline__ void acc_flush(Lit12& L, uint8_t* __restrict__ out8, uint32_t dmy) {
-#if HPK_ACC_PIPE
-    acc_pend(L, out8, dmy);
-#endif
-    if (L.o & 24u) *reinterpret_cast<uint32_t*>(out8 + ((L.o >> 3) & ~3u)) = L.acc;
-    L.o >>= 3;
-    L.acc = 0u;
-}
-__device__ __forceinline__ void lit_acc_body(Lit12& L, const uint32_t* __restrict__ win32, const uint32_t* __restrict__ lut,
-                                             const uint16_t* __restrict__ lo, uint8_t* __restrict__ out8, uint32_t dmy,
-                                             bool& body) {
-    const uint32_t d3 = win32[(L.X >> 5) + 2];
-    const uint32_t w = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-    const uint32_t e1 = lut[w >> (32 - HPK_LUT_BITS)];
-#if HPK_ACC_PIPE  // the previous step's bytes while this step's first lookup is in flight
-    HPK_SCHED_FENCE();
-    acc_pend(L, out8, dmy);
-    HPK_SCHED_FENCE();
-#endif
-    const uint32_t u1 = HPK_L4_HELD(e1);
-    const uint32_t e2 = lut[(w << u1) >> (32 - HPK_LUT_BITS)];
-    const uint32_t u2 = HPK_L4_HELD(e2);
-    const uint32_t xn = L.X + u1 + u2;
-    const bool cross = (xn ^ L.X) > 31u;
-    L.d0 = cross ? L.d1 : L.d0;
-    L.d1 = cross ? L.d2 : L.d1;
-    L.d2 = cross ? d3 : L.d2;
-    L.X = xn;
-#if HPK_ACC_PIPE
-    L.pe1 = e1;
-    L.pe2 = e2;
-#else
-    acc_put(L, (e1 & 0xFFFFu) | ((e2 & 0xFFFFu) << HPK_L4_C8(e1)), HPK_L4_C8(e1) + HPK_L4_C8(e2), out8, dmy);
-#endif
-    if (u2 == 0u) {
-#if HPK_ACC_PIPE
-        acc_pend(L, out8, dmy);
-#endif  // e2 holds no code (nor e1, if u1 == 0): a 13..30-bit code or EOS at X with > 12 bits
-                     // left (lit12_body)
-        const uint32_t wp = __builtin_amdgcn_alignbit(L.d0, L.d1, ~L.X);
-        uint32_t sy, len;
-        bool eos;
-        lo_decode(wp, lo, sy, len, eos);
-        const uint32_t r = L.Eb - L.X;
-        if (len > r) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
-            L.st = HPK_PADDING_TOO_LARGE;
-            L.Eb = L.X;
-        } else if (eos) {  // huffman.rs:112-116
-            L.st = HPK_EOS_IN_STRING;
-            L.Eb = L.X;
-        } else {
-            acc_put(L, sy, 8u, out8, dmy);
-            L.X += len;
-            lit12_load(L, win32);
-        }
-    }
-    body = L.Eb - L.X >= kBodyMin;
 }
 
 }  // namespace hpkdec

@@ -30,7 +30,6 @@ struct DecodeArgs {
     const uint32_t* lut;  // two-symbol table (hpk_code.h), step 8
     const uint32_t* lut2; // the same in the LUT2 layout (decode v12)
     const uint32_t* lut3; // the same in the LUT3 layout (decode v28, the wave kernel's long and huge phases)
-    const uint32_t* lut4; // the same in the LUT4 layout (decode v31, the wave kernel's fills)
     unsigned long long* dbg;  // diagnostic builds only: per-wave timestamps
     uint32_t in_cap, out_cap;  // blob sizes (clamped to HPK_MAX_OFFSET): larger offsets are bad
     uint32_t* err;             // sticky error flag (host-mapped): set to 1 on bad offsets

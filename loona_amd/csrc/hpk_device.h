@@ -18,7 +18,6 @@ struct hpk_ctx {
     uint32_t* d_lut = nullptr;
     uint32_t* d_lut2 = nullptr;
     uint32_t* d_lut3 = nullptr;
-    uint32_t* d_lut4 = nullptr;
     uint16_t* d_lo = nullptr;
     uint8_t* d_t8 = nullptr;
     uint32_t* d_codes = nullptr;  // [0,257) code, [257,514) length

@@ -46,31 +46,10 @@
 #ifndef HPK_LUT3
 #define HPK_LUT3 1  // v28: the wave kernel's lookups in the LUT3 layout (byte-wide "bits held")
 #endif
-#ifndef HPK_WAVE_ACC
-#define HPK_WAVE_ACC 0  // 1: body steps of fills with 4-aligned regions store one accumulated dword per step
-                        // (lit_acc_body, LUT4) instead of four bytes: measured 847-863 us against 804-821
-                        // (round 5, profiles/r05/ab_acc_dword_*rejected.jsonl, software-pipelined or not)
-#endif
 #ifndef HPK_CW_LANE_DIAG
 #define HPK_CW_LANE_DIAG 0  // (measurement only) 2: no copy loop, 3: 16-byte pieces at 16-aligned
                             // addresses, 4: no 16-byte stores
 #endif
-#ifndef HPK_TAIL2
-#define HPK_TAIL2 0  // a lane's two tails stepped in one block (lit12_step2): measured slower, config 5
-                     // 810-821 vs 802-808 us (profiles/r05/ab_tail2_rejected.jsonl)
-#endif
-#ifndef HPK_WAVE_DUAL
-#define HPK_WAVE_DUAL 0  // 1: a lane's two literals' body steps in one block (lit12_body2): bit-exact (GPU suite
-                         // 176 passed) but 1098-1105 us against 810-814 (round 5, profiles/r05/ab_dual_walk_rejected.jsonl)
-#endif
-#ifndef HPK_DUAL_UNROLL
-#define HPK_DUAL_UNROLL 2  // fused double steps between the wave's end checks
-#endif
-#ifndef HPK_WAVE_OR
-#define HPK_WAVE_OR 0  // 1: fills decode into a zeroed image by dword ORs (lit_or_body / lit_or_step, LUT4):
-                       // measured 882-899 us against 855-870 (round 5, profiles/r05/ab_or_output_rejected.jsonl)
-#endif
-
 namespace hpkdec {
 
 template <int kWinB, int kImgB>
@@ -149,16 +128,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
         reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
-    constexpr int kTab = HPK_LUT3 && HPK_BODY ? 3 : 2;  // (the long and huge phases' layout)
-    // v31: the fills' steps OR whole dwords into a zeroed image (LUT4); the long and huge phases get
-    // the LUT3 / LUT2 layout back after the fills
-    constexpr bool kOr = HPK_WAVE_OR && HPK_BODY && kMode != 1 && kMode != 2 && !(kMode >= 6 && kMode <= 10);
-    // v32: the fills' table is LUT4 (accumulated dword stores in 4-aligned fills, byte stores otherwise)
-    constexpr bool kAccOn = HPK_WAVE_ACC && HPK_BODY && !kOr && kMode != 1 && kMode != 2 && !(kMode >= 6 && kMode <= 10);
-    constexpr int kTabF = kAccOn ? 4 : kTab;
+    constexpr int kTab = HPK_LUT3 && HPK_BODY ? 3 : 2;  // the table layout of the fills and the phases after them
     for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
-        reinterpret_cast<uint4*>(s_lut)[t] =
-            reinterpret_cast<const uint4*>(kOr || kAccOn ? a.lut4 : kTab == 3 ? a.lut3 : a.lut2)[t];
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
     if (tid < 16) s_ctr[tid] = 0;
     if (kMode == 3)
         for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
@@ -256,11 +228,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         const uint32_t* const wl32 = reinterpret_cast<const uint32_t*>(smem);
         uint8_t* const ol8 = smem;
         const uint32_t dmy = obase + (uint32_t)G::kImg + lane * 4u;
-        uint32_t* const img32 = reinterpret_cast<uint32_t*>(smem);
-        if (kOr) {  // the image starts zeroed (then the write-back zeroes what it has read out)
-            uint4* l16 = reinterpret_cast<uint4*>(s_img);
-            for (uint32_t i = lane; i < (uint32_t)G::kImg / 16u; i += 64u) l16[i] = make_uint4(0u, 0u, 0u, 0u);
-        }
         // The workgroup's range is handed out in chunks, in order, to whichever wave asks next (an LDS
         // cursor): a static split left the waves the SIMDs' arbitration favours idle at the end while
         // the others finished (11 % of a wave's time). Chunks shrink as the range drains (guided
@@ -372,7 +339,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                     const uint32_t ci = c0 + lane + 64u * r;
                     if (ci < c1) {
                         if ((ci << 4) >= pG0 && (ci << 4) + 16u <= pG1) g16[ci] = l16[ci - c0];
-                        if (kOr) l16[ci - c0] = make_uint4(0u, 0u, 0u, 0u);
                     }
                 }
             }
@@ -499,7 +465,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             const uint32_t cntl = min(128u, ce - cur);
             const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
             // 1. offsets: bounds (bad), what fits
-            bool bad = false, unal = false;
+            bool bad = false;
             uint32_t ex[2], ey[2];
             bool fits[2];
             ends();
@@ -510,14 +476,12 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const uint32_t p0 = io0[r] + a.in_mis, p1 = io1[r] + a.in_mis;
                 const uint32_t o0 = oo0[r] + a.out_mis, o1 = oo1[r] + a.out_mis;
                 fits[r] = t < cntl && p1 - base16 <= (uint32_t)kWinB && o1 - ob16 <= (uint32_t)G::kImg;
-                unal |= fits[r] && ((o0 | o1) & 3u) != 0u;
                 const uint32_t nbytes = p1 - p0, ocap = o1 - o0;
                 const bool fast = ocap >= (nbytes * 8u) / 5u;
                 ex[r] = (p0 - base16) | (nbytes << 16);
                 ey[r] = t | ((o0 - ob16) << 12) | (fast ? 0u : kQ7Byte);
             }
             const bool wbad = __any(bad) || stop != 0u;
-            const bool fal = kAccOn && !__any(unal);  // every region of the fill 4-aligned (wave-uniform)
             stamp(1);
             dg_add(8, 1u);
             if (wbad) {  // the rest of the wave's chunks is void; nothing more is decoded or written here
@@ -661,11 +625,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             // (through an LDS-qualified pointer: a volatile read through a generic one is a flat load,
             // and its vmcnt(0) wait made every fill wait for its own write-back's stores)
             stop = *(volatile HPK_LDS_AS uint32_t*)(&s_ctr[0]);
-            if (kOr) {  // the counting sort's classes and the queue (image bytes [0, 1280)) zeroed again
-                uint4* l16 = reinterpret_cast<uint4*>(s_img) + (opaque(lane) - lane);
-                l16[lane] = make_uint4(0u, 0u, 0u, 0u);
-                if (lane < 16) l16[64u + lane] = make_uint4(0u, 0u, 0u, 0u);
-            }
             // 6. the next fill's offsets and window, in flight while this one decodes. Issued
             // unconditionally (past the last chunk: this fill's again, never used): under a branch the
             // registers' old and new values met in copies, and a copy waits for its load (vmcnt(0)
@@ -683,12 +642,10 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 const uint32_t o = (e.y >> 12) & 0x1FFFFu;
                 T.X = wbits + (e.x & 0xFFFFu) * 8u + 31u;
                 T.Eb = T.X + (T.act ? nb * 8u : 0u);
-                T.o = kOr ? (obase + o) * 8u : obase + o;  // (v31: in bits)
+                T.o = obase + o;
                 T.o0 = obase + o;
                 T.st = HPK_OK;
                 T.prog = false;
-                T.pe1 = T.pe2 = 0u;
-                T.acc = 0u;
                 lit12_load(T, wl32);
             };
             load(L, e1, t1);
@@ -702,128 +659,69 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 // v27: body steps (lit12_body, no fit tests) while a literal has >= kBodyMin bits left,
                 // slot t1's body then slot t2's; then the checked steps (lit12_step) for the two
                 // literals' last bits, t1's tail then t2's. A lane's first literal waits between the
-                // two phases as (aX, aO, aSt). v32 (kA, fills whose regions are all 4-aligned): the body
-                // steps store accumulated dwords (lit_acc_body; L.o in bits while the body runs, the
-                // part-filled dword stored by acc_flush when it ends)
-                auto bodywalk = [&](auto acc_tag) {
-                    constexpr bool kA = decltype(acc_tag)::value;
-                    bool body = L.Eb - L.X >= kBodyMin;
-                    if (kA) L.o <<= 3;
-                    uint32_t aX = L.X, aO = L.o, aSt = L.st;
-                    bool aAct = L.act, onA = true;
-                    for (;;) {
-                        dg_add(9, 1u);
+                // two phases as (aX, aO, aSt). (Measured and not taken, round 5: accumulated dword
+                // stores, dword ORs, both bodies or both tails in one block)
+                bool body = L.Eb - L.X >= kBodyMin;
+                uint32_t aX = L.X, aO = L.o, aSt = L.st;
+                bool aAct = L.act, onA = true;
+                for (;;) {
+                    dg_add(9, 1u);
 #pragma unroll
-                        for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
-                            if (body && kOr)
-                                lit_or_body(L, wl32, s_lut, s_lo, img32, body);
-                            else if (body && kA)
-                                lit_acc_body(L, wl32, s_lut, s_lo, ol8, dmy, body);
-                            else if (body)
-                                lit12_body<kStore, kTabF, (kMode >= 8 && kMode <= 10) ? kMode - 7 : 0>(L, wl32, s_lut, s_lo,
-                                                                                                        ol8, body);
-                            if (kMode == 6) {
+                    for (int s = 0; s < HPK_BODY_UNROLL; ++s) {
+                        if (body)
+                            lit12_body<kStore, kTab, (kMode >= 8 && kMode <= 10) ? kMode - 7 : 0>(L, wl32, s_lut, s_lo, ol8,
+                                                                                                   body);
+                        if (kMode == 6) {
 #pragma unroll
-                                for (int q = 0; q < 4; ++q) {
-                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[0]) : "v"(L.X));
-                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[1]) : "v"(L.o));
-                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[2]) : "v"(L.Eb));
-                                    asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[3]) : "v"(L.d1));
-                                }
+                            for (int q = 0; q < 4; ++q) {
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[0]) : "v"(L.X));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[1]) : "v"(L.o));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[2]) : "v"(L.Eb));
+                                asm volatile("v_xor_b32 %0, %0, %1" : "+v"(sens[3]) : "v"(L.d1));
                             }
                         }
-                        if (__any(!body)) {
-                            const bool sw = !body & onA;
-                            if (sw) {  // the first literal's body is done: it waits, the second one starts (its
-                                       // state made from the queue entry here, not carried through the loop)
-                                if (kOr) lit_or_pend(L, img32);
-                                if (kA) acc_flush(L, ol8, dmy);
-                                aX = L.X;
-                                aO = L.o;
-                                aSt = L.st;
-                                aAct = L.act;
-                                load(L, e2, t2);
-                                if (kA) L.o <<= 3;
-                                onA = false;
-                                body = L.Eb - L.X >= kBodyMin;
-                            }
-                            if (!__any(body)) break;
+                    }
+                    if (__any(!body)) {
+                        const bool sw = !body & onA;
+                        if (sw) {  // the first literal's body is done: it waits, the second one starts (its
+                                   // state made from the queue entry here, not carried through the loop)
+                            aX = L.X;
+                            aO = L.o;
+                            aSt = L.st;
+                            aAct = L.act;
+                            load(L, e2, t2);
+                            onA = false;
+                            body = L.Eb - L.X >= kBodyMin;
                         }
+                        if (!__any(body)) break;
                     }
-                    // tails: both literals of the lane at once, t1's from where its body stopped (restored
-                    // into L), t2's (in N) from where its body stopped; a step that proves the walk has
-                    // ended clears `more`, so no step is spent finding out (usually one step per tail)
-                    if (kOr) lit_or_pend(L, img32);
-                    if (kA) acc_flush(L, ol8, dmy);
-                    N = L;
-                    L.X = aX;
-                    L.o = aO;
-                    L.st = aSt;
-                    L.act = aAct;
-                    L.Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (aAct ? (e1.x >> 16) * 8u : 0u);
-                    L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);  // (bytes; L.o in bits when kOr)
-                    L.idx = e1.y & 0xFFFu;
-                    if (aSt != HPK_OK) L.Eb = L.X;  // ended in its body (EOS / padding): no tail
-                    lit12_load(L, wl32);
-                    L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
-                    N.more = N.Eb - N.X >= 5u;
-                    while (__any(L.more | N.more)) {
-                        if (kOr) {
-                            if (L.more) lit_or_step(L, wl32, s_lut, s_lo, img32);
-                            if (N.more) lit_or_step(N, wl32, s_lut, s_lo, img32);
-                        } else if (HPK_TAIL2) {  // both tails in one block (off)
-                            lit12_step2<kStore, true, kTabF>(L, N, wl32, s_lut, s_lo, ol8, dmy);
-                        } else {
-                            if (L.more) lit12_step<kStore, true, kTabF, true>(L, wl32, s_lut, s_lo, ol8, dmy);
-                            if (N.more) lit12_step<kStore, true, kTabF, true>(N, wl32, s_lut, s_lo, ol8, dmy);
-                        }
-                    }
-                    // results in the v26 form: the first slot's end state saved, the second in L
-                    sX = L.X;
-                    sO = kOr ? L.o >> 3 : L.o;
-                    sSt = L.st;
-                    s1 = L.act;
-                    L = N;
-                    Lend = kOr ? L.o >> 3 : L.o;
-                };
-#if HPK_WAVE_DUAL
-                // v32: both literals' bodies stepped together (lit12_body2), then both tails
-                auto dualwalk = [&]() {
-                    load(N, e2, t2);
-                    bool bl = L.Eb - L.X >= kBodyMin, bn = N.Eb - N.X >= kBodyMin;
-                    while (__any(bl | bn)) {
-                        dg_add(9, 1u);
-#pragma unroll
-                        for (int s = 0; s < HPK_DUAL_UNROLL; ++s)
-                            lit12_body2<kStore, kTabF>(L, N, wl32, s_lut, s_lo, ol8, dmy, bl, bn);
-                    }
-                    if (L.st != HPK_OK) L.Eb = L.X;  // (ended in its body: no tail)
-                    if (N.st != HPK_OK) N.Eb = N.X;
-                    L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
-                    N.more = N.Eb - N.X >= 5u;
-                    while (__any(L.more | N.more)) {
-                        if (L.more) lit12_step<kStore, true, kTabF, true>(L, wl32, s_lut, s_lo, ol8, dmy);
-                        if (N.more) lit12_step<kStore, true, kTabF, true>(N, wl32, s_lut, s_lo, ol8, dmy);
-                    }
-                    sX = L.X;
-                    sO = L.o;
-                    sSt = L.st;
-                    s1 = L.act;
-                    L = N;
-                    Lend = L.o;
-                };
-                if (kMode == 0 || kMode == 3) {
-                    dualwalk();
-                } else
-#endif
-                if constexpr (kAccOn) {
-                    if (fal)
-                        bodywalk(std::integral_constant<bool, true>{});
-                    else
-                        bodywalk(std::integral_constant<bool, false>{});
-                } else {
-                    bodywalk(std::integral_constant<bool, false>{});
                 }
+                // tails: both literals of the lane at once, t1's from where its body stopped (restored
+                // into L), t2's (in N) from where its body stopped; a step that proves the walk has
+                // ended clears `more`, so no step is spent finding out (usually one step per tail)
+                N = L;
+                L.X = aX;
+                L.o = aO;
+                L.st = aSt;
+                L.act = aAct;
+                L.Eb = wbits + (e1.x & 0xFFFFu) * 8u + 31u + (aAct ? (e1.x >> 16) * 8u : 0u);
+                L.o0 = obase + ((e1.y >> 12) & 0x1FFFFu);
+                L.idx = e1.y & 0xFFFu;
+                if (aSt != HPK_OK) L.Eb = L.X;  // ended in its body (EOS / padding): no tail
+                lit12_load(L, wl32);
+                L.more = L.Eb - L.X >= 5u;  // (fewer bits than the shortest code: ended)
+                N.more = N.Eb - N.X >= 5u;
+                while (__any(L.more | N.more)) {
+                    if (L.more) lit12_step<kStore, true, kTab, true>(L, wl32, s_lut, s_lo, ol8, dmy);
+                    if (N.more) lit12_step<kStore, true, kTab, true>(N, wl32, s_lut, s_lo, ol8, dmy);
+                }
+                // results in the v26 form: the first slot's end state saved, the second in L
+                sX = L.X;
+                sO = L.o;
+                sSt = L.st;
+                s1 = L.act;
+                L = N;
+                Lend = L.o;
             } else if (kMode != 1) {
                 for (;;) {
                     dg_add(9, 1u);
@@ -926,11 +824,6 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     // ---- the literals left to the long-literal phase ----
     __syncthreads();  // every wave's fills, list entries and stores are out
     const uint32_t c1 = s_ctr[1], c2 = s_ctr[2], nh = min(s_ctr[8], kHugeMax);
-    if ((kOr || kAccOn) && c1 + c2 + nh != 0u) {  // (block-uniform) the phases' table layout
-        for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
-            reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
-        __syncthreads();
-    }
     huge_phase<G::kBlock, kTab>(a, s_huge, nh, reinterpret_cast<uint32_t*>(smem + G::kWaveOff), s_lut, s_lo);
     if (c1 + c2) {
         static_assert(G::kWaveOff % 16 == 0, "long-phase rings");

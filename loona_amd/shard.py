@@ -139,9 +139,11 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None, co
     `balanced_ranges`. Shard s is decoded on rank owner(s, world); root keeps its own.
     decode_fn(blob, off) -> (out_blob, out_off, out_len int32/uint32, status uint8) on `device`.
     compacted: decode_fn is the compacted form (HuffmanCodec.decode_compact, hpk_decode_batch_compact):
-    its out_blob[:out_off[m]] already holds every literal's bytes, literal i at out_off[i], so the owner
-    sends that span and the offsets as they are (no gather pass); root's offsets are then those starts
-    (not monotone) with [m] = the span's length.
+    literal i's bytes are at out_off[i] (starts, not regions: not monotone), and out_blob[:out_off[m]] is
+    the span the decode wrote. With the wave-fill kernel (batches of >= 4M literals) that span holds
+    unwritten gaps between its workgroups' shares (~1.3x the decoded bytes on a config-5 shard), so the
+    owner gathers the decoded bytes end to end exactly as for the region form (`compact` takes any
+    per-literal starts) and only decoded bytes travel; root's offsets are their exclusive sum either way.
 
     Everything stays in device memory when `device` is a GPU (RCCL point-to-point over xGMI; no host
     copy of the data): the shard sizes go out with one broadcast and the offsets and blob of each
@@ -219,8 +221,7 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None, co
             m = sizes[s][0]
             if compacted:
                 _check(oo, f"shard {s} out_off", ("int32", "uint32"))
-                tot[s] = oo[m].to(torch.int64) & 0xFFFFFFFF  # the written span
-            elif m:
+            if m:
                 tot[s] = ol[:m].to(torch.int64).sum()
     except Exception as e:  # noqa: BLE001 -- re-raised after the collective
         err = e
@@ -233,11 +234,9 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None, co
         if err is not None:
             raise err
         raise RuntimeError(f"scatter_decode_gather: {totals[S]} rank(s) failed to decode their shards")
-    # 5. the owners lay their shards' bytes end to end; bytes, out_len and status go to root
-    if compacted:
-        packed = {s: res[s][0][: int(totals[s])] for s in mine}
-    else:
-        packed = {s: compact(*res[s][:3], sizes[s][0], int(totals[s])) for s in mine}
+    # 5. the owners lay their shards' bytes end to end (region starts or compacted starts alike); bytes,
+    # out_len and status go to root
+    packed = {s: compact(*res[s][:3], sizes[s][0], int(totals[s])) for s in mine}
     out, ops = {}, []
     for s in range(S):
         o = owner(s, world)
@@ -247,8 +246,6 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None, co
         if rank == o:
             ol, st = res[s][2], res[s][3]
             ops += [(dist.isend, _wire(ol[:m]), root), (dist.isend, st[:m], root)]
-            if compacted:
-                ops.append((dist.isend, _wire(res[s][1][: m + 1]), root))
             if nbytes:
                 ops.append((dist.isend, packed[s], root))
         elif rank == root:
@@ -256,13 +253,9 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None, co
             st = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
             cb = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
             ops += [(dist.irecv, ol[:m], o), (dist.irecv, st[:m], o)]
-            co = None
-            if compacted:
-                co = torch.empty(m + 1, dtype=torch.int32, device=dev)
-                ops.append((dist.irecv, co, o))
             if nbytes:
                 ops.append((dist.irecv, cb[:nbytes], o))
-            out[s] = (cb[:nbytes], ol[:m], st[:m], co)
+            out[s] = (cb[:nbytes], ol[:m], st[:m])
     ops = [x for x in ops if x[1].numel()]
     _p2p(dist, ops, group)
     if rank != root:
@@ -272,9 +265,7 @@ def scatter_decode_gather(shards, decode_fn, group=None, root=0, device=None, co
         m = sizes[s][0]
         if s in mine:
             cb, ol, st = packed[s], res[s][2][:m], res[s][3][:m]
-            co = res[s][1][: m + 1] if compacted else None
         else:
-            cb, ol, st, co = out[s]
-        offs = (co.to(torch.int64) & 0xFFFFFFFF) if compacted else compact_offsets(ol, m)
-        result.append((cb, offs, ol, st))
+            cb, ol, st = out[s]
+        result.append((cb, compact_offsets(ol, m), ol, st))
     return result

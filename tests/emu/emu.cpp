@@ -73,7 +73,7 @@ static int run_lanes(std::mt19937_64& rng, int nlit, int maxlen) {
         std::vector<uint8_t> img(op + 256 + 64, 0xEE);
         const uint32_t dmy = op + 64 + 4;  // the lane's dummy dword, past the regions
         std::vector<uint32_t> olen(k), ost(k);
-        const uint32_t* lut = kTab == 4 ? T.lut4 : kTab == 3 ? T.lut3 : T.lut2;
+        const uint32_t* lut = kTab == 3 ? T.lut3 : T.lut2;
         for (int lane = 63; lane >= 0; --lane) {
             const uint32_t t1 = lane, t2 = 127 - lane;
             auto load = [&](Lit12& Z, uint32_t tt) {
@@ -124,183 +124,6 @@ static int run_lanes(std::mt19937_64& rng, int nlit, int maxlen) {
         for (uint32_t j = op; j < op + 64; ++j)
             if (img[j] != 0xEE) {
                 if (bad < 5) printf("lanes tab %d: byte %u past the last region written\n", kTab, j);
-                ++bad;
-                break;
-            }
-    }
-    return bad;
-}
-
-// The wave kernel's v32 lane protocol in fills whose regions are all 4-aligned: body steps with
-// accumulated dword stores (lit_acc_body, L.o in bits, acc_flush at the body's end), then the checked
-// LUT4 tails (lit12_step<.., 4, true>) with byte stores. Regions are the decoded bound rounded up to 4,
-// back to back from a 4-aligned start, lanes in reverse order; nothing may land past the last region.
-static int run_lanes_acc(std::mt19937_64& rng, int nlit, int maxlen) {
-    auto lits = make_lits(rng, nlit, maxlen);
-    int bad = 0;
-    for (size_t f = 0; f < lits.size(); f += 128) {
-        const size_t k = std::min<size_t>(128, lits.size() - f);
-        const uint32_t mis = rng() % 16;
-        std::vector<uint8_t> win(mis);
-        std::vector<uint32_t> p0(k), nb(k), o0(k), cap(k);
-        uint32_t op = 4 * (rng() % 4);
-        for (size_t t = 0; t < k; ++t) {
-            p0[t] = win.size();
-            nb[t] = lits[f + t].size();
-            win.insert(win.end(), lits[f + t].begin(), lits[f + t].end());
-            o0[t] = op;
-            cap[t] = (nb[t] * 8 / 5 + 3) & ~3u;
-            op += cap[t];
-        }
-        win.resize(win.size() + 64, 0x5A);
-        std::vector<uint32_t> w32(win.size() / 4 + 4, 0);
-        for (size_t j = 0; j + 4 <= win.size(); j += 4)
-            w32[j / 4] = ((uint32_t)win[j] << 24) | ((uint32_t)win[j + 1] << 16) | ((uint32_t)win[j + 2] << 8) | win[j + 3];
-        std::vector<uint32_t> img32((op + 256 + 64) / 4 + 1, 0xEEEEEEEEu);
-        uint8_t* img = reinterpret_cast<uint8_t*>(img32.data());
-        const uint32_t dmy = op + 64 + 4;  // the lane's dummy dword, past the regions
-        std::vector<uint32_t> olen(k), ost(k);
-        for (int lane = 63; lane >= 0; --lane) {
-            const uint32_t t1 = lane, t2 = 127 - lane;
-            auto load = [&](Lit12& Z, uint32_t tt) {
-                const uint32_t u = std::min<uint32_t>(tt, k - 1);
-                Z.act = tt < k;
-                Z.idx = tt;
-                Z.X = p0[u] * 8u + 31u;
-                Z.Eb = Z.X + (Z.act ? nb[u] * 8u : 0u);
-                Z.o = o0[u] * 8u;
-                Z.o0 = o0[u];
-                Z.st = HPK_OK;
-                Z.prog = false;
-                Z.pe1 = Z.pe2 = 0u;
-                Z.acc = 0u;
-                lit12_load(Z, w32.data());
-            };
-            Lit12 L, N;
-            load(L, t1);
-            load(N, t2);
-            bool body = L.Eb - L.X >= kBodyMin;
-            while (body) lit_acc_body(L, w32.data(), T.lut4, T.lo, img, dmy, body);
-            acc_flush(L, img, dmy);
-            Lit12 A = L;
-            L = N;
-            body = L.Eb - L.X >= kBodyMin;
-            while (body) lit_acc_body(L, w32.data(), T.lut4, T.lo, img, dmy, body);
-            acc_flush(L, img, dmy);
-            N = L;
-            L = A;
-            const uint32_t u1 = std::min<uint32_t>(t1, k - 1);
-            L.Eb = L.st != HPK_OK ? L.X : p0[u1] * 8u + 31u + (L.act ? nb[u1] * 8u : 0u);
-            lit12_load(L, w32.data());
-            L.more = L.Eb - L.X >= 5u;
-            N.more = N.Eb - N.X >= 5u;
-            for (int guard = 0; (L.more || N.more) && guard < 1000000; ++guard) {
-                if (L.more) lit12_step<kPred, true, 4, true>(L, w32.data(), T.lut4, T.lo, img, dmy);
-                if (N.more) lit12_step<kPred, true, 4, true>(N, w32.data(), T.lut4, T.lo, img, dmy);
-            }
-            if (L.act) olen[t1] = L.o - L.o0, ost[t1] = lit12_status(L);
-            if (N.act) olen[t2] = N.o - N.o0, ost[t2] = lit12_status(N);
-        }
-        for (size_t t = 0; t < k; ++t) {
-            std::vector<uint8_t> ref(cap[t] + 8);
-            size_t rl = 0;
-            const int rs = oracle_decode(lits[f + t].data(), nb[t], ref.data(), ref.size(), &rl);
-            const bool ok = rs == (int)ost[t] && rl == olen[t] && memcmp(ref.data(), img + o0[t], rl) == 0;
-            if (!ok && bad < 5)
-                printf("lanes acc: literal %zu (%u B): status %u vs %d, length %u vs %zu\n", f + t, nb[t], ost[t], rs, olen[t], rl);
-            bad += !ok;
-        }
-        for (uint32_t j = op; j < op + 64; ++j)
-            if (img[j] != 0xEE) {
-                if (bad < 5) printf("lanes acc: byte %u past the last region written\n", j);
-                ++bad;
-                break;
-            }
-    }
-    return bad;
-}
-
-// The wave kernel's v31 lane protocol: lit_or_body / lit_or_step (LUT4) OR whole dwords into a zeroed
-// image; regions back to back at any byte alignment, lanes in reverse order. Every image byte outside
-// the decoded bytes must stay zero (an OR of a stray byte would show there).
-static int run_lanes_or(std::mt19937_64& rng, int nlit, int maxlen) {
-    auto lits = make_lits(rng, nlit, maxlen);
-    int bad = 0;
-    for (size_t f = 0; f < lits.size(); f += 128) {
-        const size_t k = std::min<size_t>(128, lits.size() - f);
-        const uint32_t mis = rng() % 16;
-        std::vector<uint8_t> win(mis);
-        std::vector<uint32_t> p0(k), nb(k), o0(k), cap(k);
-        uint32_t op = rng() % 16;
-        for (size_t t = 0; t < k; ++t) {
-            p0[t] = win.size();
-            nb[t] = lits[f + t].size();
-            win.insert(win.end(), lits[f + t].begin(), lits[f + t].end());
-            o0[t] = op;
-            cap[t] = nb[t] * 8 / 5;
-            op += cap[t];
-        }
-        win.resize(win.size() + 64, 0x5A);
-        std::vector<uint32_t> w32(win.size() / 4 + 4, 0);
-        for (size_t j = 0; j + 4 <= win.size(); j += 4)
-            w32[j / 4] = ((uint32_t)win[j] << 24) | ((uint32_t)win[j + 1] << 16) | ((uint32_t)win[j + 2] << 8) | win[j + 3];
-        std::vector<uint32_t> img32(op / 4 + 64, 0);
-        const uint8_t* img = reinterpret_cast<const uint8_t*>(img32.data());
-        std::vector<uint32_t> olen(k), ost(k);
-        for (int lane = 63; lane >= 0; --lane) {
-            const uint32_t t1 = lane, t2 = 127 - lane;
-            auto load = [&](Lit12& Z, uint32_t tt) {
-                const uint32_t u = std::min<uint32_t>(tt, k - 1);
-                Z.act = tt < k;
-                Z.idx = tt;
-                Z.X = p0[u] * 8u + 31u;
-                Z.Eb = Z.X + (Z.act ? nb[u] * 8u : 0u);
-                Z.o = o0[u] * 8u;
-                Z.o0 = o0[u];
-                Z.st = HPK_OK;
-                Z.prog = false;
-                Z.pe1 = Z.pe2 = 0u;
-                lit12_load(Z, w32.data());
-            };
-            Lit12 L, N;
-            load(L, t1);
-            load(N, t2);
-            bool body = L.Eb - L.X >= kBodyMin;
-            while (body) lit_or_body(L, w32.data(), T.lut4, T.lo, img32.data(), body);
-            lit_or_pend(L, img32.data());
-            Lit12 A = L;
-            L = N;
-            body = L.Eb - L.X >= kBodyMin;
-            while (body) lit_or_body(L, w32.data(), T.lut4, T.lo, img32.data(), body);
-            lit_or_pend(L, img32.data());
-            N = L;
-            L = A;
-            const uint32_t u1 = std::min<uint32_t>(t1, k - 1);
-            L.Eb = L.st != HPK_OK ? L.X : p0[u1] * 8u + 31u + (L.act ? nb[u1] * 8u : 0u);
-            lit12_load(L, w32.data());
-            L.more = L.Eb - L.X >= 5u;
-            N.more = N.Eb - N.X >= 5u;
-            for (int guard = 0; (L.more || N.more) && guard < 1000000; ++guard) {
-                if (L.more) lit_or_step(L, w32.data(), T.lut4, T.lo, img32.data());
-                if (N.more) lit_or_step(N, w32.data(), T.lut4, T.lo, img32.data());
-            }
-            if (L.act) olen[t1] = (L.o >> 3) - L.o0, ost[t1] = lit12_status(L);
-            if (N.act) olen[t2] = (N.o >> 3) - N.o0, ost[t2] = lit12_status(N);
-        }
-        std::vector<uint8_t> mine(img32.size() * 4, 0);
-        for (size_t t = 0; t < k; ++t) {
-            std::vector<uint8_t> ref(cap[t] + 8);
-            size_t rl = 0;
-            const int rs = oracle_decode(lits[f + t].data(), nb[t], ref.data(), ref.size(), &rl);
-            const bool ok = rs == (int)ost[t] && rl == olen[t] && memcmp(ref.data(), img + o0[t], rl) == 0;
-            if (!ok && bad < 5)
-                printf("lanes or: literal %zu (%u B): status %u vs %d, length %u vs %zu\n", f + t, nb[t], ost[t], rs, olen[t], rl);
-            bad += !ok;
-            for (uint32_t j = 0; j < olen[t] && o0[t] + j < mine.size(); ++j) mine[o0[t] + j] = 1;
-        }
-        for (size_t j = 0; j < mine.size(); ++j)
-            if (!mine[j] && img[j] != 0) {
-                if (bad < 5) printf("lanes or: image byte %zu outside the decoded bytes is %u\n", j, img[j]);
                 ++bad;
                 break;
             }
@@ -427,9 +250,6 @@ int main(int argc, char** argv) {
         bad += run_lanes<3, true>(rng, 3000, maxlen);
         bad += run_lanes<2, true>(rng, 3000, maxlen);
         bad += run_lanes<2, false>(rng, 3000, maxlen);
-        bad += run_lanes_or(rng, 3000, maxlen);
-        bad += run_lanes<4, true>(rng, 3000, maxlen);
-        bad += run_lanes_acc(rng, 3000, maxlen);
     }
     long fixes = 0;
     bad += run_huge(rng, iters * 3, 1024, &fixes);

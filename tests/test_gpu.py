@@ -1063,6 +1063,8 @@ def test_compact_two_streams_overlap(codec):
     generated strings, and the layouts must be disjoint and inside each call's capacity."""
     from loona_amd import HuffmanCodec, synth
 
+    if codec.variant != "fill":
+        pytest.skip("runs once (its own context, auto kernel selection): the fill variant's run")
     big = synth.device_config2(codec, n=2_000_000, seed=101)
     small = synth.device_config2(codec, n=20_000, seed=202)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
@@ -1078,6 +1080,45 @@ def test_compact_two_streams_overlap(codec):
             for w, (out, oo, ol, st) in ((big, r1), (small, r2)):
                 _check_compact(out, oo, ol, w.n)
                 synth.check_decoded(w, out, oo, ol, st)
+
+
+@pytest.mark.parametrize("kernel", ["fill", "wave"])
+def test_first_call_on_foreign_stream_then_slot_reuse(codec, kernel):
+    """a context whose FIRST call runs on a stream it does not own, followed by calls on 9
+    more streams, so that the 8 per-stream slots (long-literal list, bound layout, cursor) are all taken
+    and the oldest one -- the foreign stream's, still decoding a large batch -- is reused. The slot's
+    recorded event must survive the switch to multi-stream mode, so the reuse waits for the large
+    decode instead of resetting its cursor or list under it. Both compacted forms (the fill kernel's
+    device cursor, the wave kernel's per-workgroup shares) and the region form; every output checked
+    byte for byte against the generated strings."""
+    from loona_amd import HuffmanCodec, synth
+
+    if codec.variant != "fill":
+        pytest.skip("runs once per kernel, on its own context")
+    big = synth.device_config3(codec, n=300_000, seed=303)  # long literals: the long-literal list is used
+    small = [synth.device_config2(codec, n=5_000 + 997 * k, seed=400 + k) for k in range(9)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(10)]
+    with HuffmanCodec(0, stream="own") as c:
+        c.set_decode_kernel(kernel)
+        for compact in (True, False):
+            c.set_stream(streams[0])
+            if compact:
+                r0 = c.decode_compact(big.enc_blob, big.enc_off, sync=False)
+            else:
+                r0 = c.decode_device(big.enc_blob, big.enc_off, sync=False)
+            rs = []
+            for k, w in enumerate(small):
+                c.set_stream(streams[k + 1])
+                rs.append(c.decode_compact(w.enc_blob, w.enc_off, sync=False) if compact
+                          else c.decode_device(w.enc_blob, w.enc_off, sync=False))
+            torch.cuda.synchronize()
+            c.check()
+            for w, (out, oo, ol, st) in [(big, r0)] + list(zip(small, rs)):
+                if compact:
+                    _check_compact(out, oo, ol, w.n)
+                synth.check_decoded(w, out, oo, ol, st)
+        c.set_stream(torch.cuda.current_stream())
 
 
 @pytest.mark.parametrize("n", [0, 1, 4095, 4096, 4097, 300_001, 16_781_313])

@@ -83,20 +83,22 @@ def _cpu_decode(b, o):
 
 def _cpu_decode_compacted(b, o):
     """A stand-in for the compacted form on CPU tensors: the CPU batch decode, then the literals' bytes
-    packed back to back in runs of 7 taken in reverse order (as the device's completion order would
-    scatter them), out_off = each literal's start, out_off[m] = the span written."""
+    packed in runs of 7 taken in reverse order (as the device's completion order would scatter them),
+    with an unwritten gap of 0xEE bytes after every run (the wave kernel's per-workgroup shares),
+    out_off = each literal's start, out_off[m] = the span written."""
     import torch
 
     ob, oo, ol, st = decode_batch_cpu(b.numpy(), o.numpy().view(np.uint32), nthreads=2)
     m = len(ol)
     starts = np.zeros(m + 1, np.int64)
-    out = np.zeros(max(int(ol.sum()), 1), np.uint8)
+    out = np.full(max(int(ol.sum()) + 5 * (m // 7 + 1), 1), 0xEE, np.uint8)
     pos = 0
     for r0 in reversed(range(0, m, 7)):
         for i in range(r0, min(m, r0 + 7)):
             starts[i] = pos
             out[pos : pos + int(ol[i])] = ob[int(oo[i]) : int(oo[i]) + int(ol[i])]
             pos += int(ol[i])
+        pos += 5  # the gap
     starts[m] = pos
     return (torch.from_numpy(out), torch.from_numpy(starts.astype(np.int32)), torch.from_numpy(ol.view(np.int32)),
             torch.from_numpy(st))
@@ -129,8 +131,9 @@ def _worker(rank, world, port, n, seed, nshards, q, compacted=False):
 
 
 def test_scatter_decode_gather_gloo_compacted():
-    """The same over gloo with a compacted decode (scatter_decode_gather(compacted=True)): each owner's
-    written span and its per-literal starts travel as they are; root's results equal the oracle's."""
+    """The same over gloo with a compacted decode (scatter_decode_gather(compacted=True)) whose span has
+    unwritten gaps: each owner gathers the decoded bytes end to end, so exactly the decoded bytes travel
+    (no gap byte reaches root) and root's offsets are their exclusive sum; results equal the oracle's."""
     import torch.multiprocessing as mp
 
     n, seed, world, nshards = 12000, 6, 2, 3
@@ -147,7 +150,8 @@ def test_scatter_decode_gather_gloo_compacted():
     blob, off = _lits(n, seed)
     b = shard.balanced_ranges(off, nshards)
     for r, (cb, coff, ol, st) in enumerate(res):
-        assert int(coff[-1]) == cb.size
+        assert int(coff[-1]) == cb.size == int(ol.view(np.uint32).astype(np.int64).sum())
+        assert (np.diff(coff) >= 0).all()
         sb, so = shard.shard(blob, off, int(b[r]), int(b[r + 1]))
         got = (cb if cb.size else np.zeros(1, np.uint8), coff.astype(np.uint32), ol.view(np.uint32), st)
         compare_batches(got, oracle_decode_batch(sb, so), f"compacted shard {r}")
