@@ -290,6 +290,47 @@ def run_compact(codec, w, stream, pmc_dir, reps=10):
     return res
 
 
+def run_host_inclusive(codec, w, reps=10):
+    """The rate including the copies (north_star: the path starts and ends in host memory): config 2's 1M
+    literals from host numpy buffers through hpk_decode_batch(HPK_PTR_HOST) -- H2D of in_blob + in_off +
+    out_off, the kernel, D2H of out_blob + out_len + status, pipelined in chunks on three streams by the
+    library -- from pageable buffers and from the same buffers page-locked (hpk_host_register, as buffet's
+    arena would be). Every call's lengths and statuses checked; never `value`."""
+    from loona_amd import _lib
+    from loona_amd.batch import decode_offsets_np
+
+    L = _lib.lib()
+    blob = np.ascontiguousarray(w.enc_blob.cpu().numpy())
+    io = np.ascontiguousarray(w.enc_off.cpu().numpy().view(np.uint32))
+    oo = decode_offsets_np(io)
+    out = np.zeros(int(oo[-1]) + 16, np.uint8)
+    ol = np.zeros(w.n, np.uint32)
+    st = np.zeros(w.n, np.uint8)
+    want = (w.dec_off[1:] - w.dec_off[:-1]).cpu().numpy().astype(np.int64)
+    moved = blob.nbytes + io.nbytes + oo.nbytes + int(oo[-1]) + ol.nbytes + st.nbytes
+    res = {"literals": w.n, "encoded_bytes": w.enc_bytes, "host_bytes_moved_per_call": int(moved), "calls": reps}
+    for mode in ("pageable", "page_locked"):
+        regs = []
+        if mode == "page_locked":
+            for arr in (blob, io, oo, out, ol, st):
+                _lib.check(L.hpk_host_register(arr.ctypes.data, arr.nbytes), "hpk_host_register")
+                regs.append(arr)
+        try:
+            codec.decode_into(blob, io, out, oo, ol, st, device=False)  # warm (scratch, streams)
+            ok = True
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                codec.decode_into(blob, io, out, oo, ol, st, device=False)
+            dt = (time.perf_counter() - t0) / reps
+            ok = bool(np.array_equal(ol.astype(np.int64), want) and not st.any())
+        finally:
+            for arr in regs:
+                _lib.check(L.hpk_host_unregister(arr.ctypes.data), "hpk_host_unregister")
+        res[mode] = {"ms_per_call": round(dt * 1e3, 3), "encoded_GiB_s": round(w.enc_bytes / dt / 2**30, 3),
+                     "pcie_GB_s": round(moved / dt / 1e9, 2), "checked": ok}
+    return res
+
+
 def run_config3(codec, stream, dev, reps=10):
     """BASELINE config 3: 1M mixed literals (Zipf(1.1) lengths 8..4096, 5 % uniform bytes), device
     encode and device decode timed apart, each over `reps` back-to-back launches; the round trip is
@@ -666,6 +707,7 @@ def main():
             "algorithmic_bytes_per_launch": a2, "roofline_frac": round(a2 / (t2 / k2) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(os.path.join(args.pmc_dir, "pmc_config2.json"), "config2", w2.n, source_hash()),
             "note": "1M literals, 4 rotating input/output copies (> 256 MiB Infinity Cache), 100 launches"}
+        line["host_inclusive"] = run_host_inclusive(codec, w2)
         cpu_w = w2
     elif rank == 0:
         cpu_w = units[0][0]

@@ -762,20 +762,56 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
                     s_ctr[11] = 0;
                     s_ctr[10] = 0;
                 }
+                if (tid < 64) s_hist[tid] = 0;  // (round 6) LPT classes: counts [0, 32), then cursors
                 lds_barrier();
+                // round 6: the list in LPT order (lpt_class_of, longest first) by a counting sort: the long phase
+                // takes it front to back, so the longest jobs start first; huge literals to the huge list
                 bool no = false;
                 for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
                     const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1], q0 = a.out_off[i], q1 = a.out_off[i + 1];
                     const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
                                     (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
-                    if (ok)
-                        leave(i, p1 - p0);
-                    else
+                    if (!ok) {
                         no = true;
+                        continue;
+                    }
+                    const uint32_t nb = p1 - p0;
+                    bool huge = false;
+                    if (nb >= HPK_HUGE_MIN && nb < kHugeLimit) {
+                        const uint32_t hh = atomicAdd(&s_ctr[11], 1u);
+                        if (hh < kHugeMax) {
+                            s_huge[hh] = i;
+                            huge = true;
+                        }
+                    }
+                    if (!huge) atomicAdd(&s_hist[lpt_class_of(nb)], 1u);
                 }
                 if (__any(no) && lane == 0) s_ctr[10] = 1u;
                 lds_barrier();
                 if (s_ctr[10] == 0) {
+                    if (tid < 64) {  // class bases
+                        const uint32_t v = tid < 32 ? s_hist[tid] : 0u;
+                        uint32_t x = v;
+#pragma unroll
+                        for (int d = 1; d < 64; d <<= 1) {
+                            const uint32_t y = __shfl_up(x, d);
+                            if (lane >= (uint32_t)d) x += y;
+                        }
+                        if (tid < 32) s_hist[32 + tid] = x - v;
+                        if (tid == 31) {
+                            s_ctr[6] = x;  // all from the front of the list
+                            s_ctr[7] = 0;
+                        }
+                    }
+                    lds_barrier();
+                    const uint32_t nh = min(s_ctr[11], kHugeMax);
+                    for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
+                        const uint32_t nb = a.in_off[i + 1] - a.in_off[i];
+                        bool huge = false;
+                        if (nb >= HPK_HUGE_MIN && nb < kHugeLimit)
+                            for (uint32_t hh = 0; hh < nh; ++hh) huge |= s_huge[hh] == i;
+                        if (!huge) a.long_list[BA + atomicAdd(&s_hist[32 + lpt_class_of(nb)], 1u)] = i;
+                    }
                     cur = BB;  // all listed
                     break;
                 }
@@ -1114,13 +1150,16 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         // lengths (all free once the fills are done)
         constexpr int kLB = HPK_LONG_WAVES * 64;
         constexpr int kLQ = kLB * (HPK_LONG_RING * 4 + HPK_LONG_OS);
-        static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
+        constexpr int kLX = kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16;   // queue extra words
+        constexpr int kLR = kLX + HPK_LONG_WAVES * HPK_LONG_CLAIM * 4;    // split records
+        static_assert(kLR + HPK_LONG_WAVES * 64 * 36 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
                           kW % 16 == 0 && kLQ % 16 == 0 && G::kHistOff == G::kInOff + kW + kO + 12 * kQ,
                       "long-phase LDS");
         long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, 2,
                    kCompact>(
             a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + kLB * HPK_LONG_RING * 4,
-            reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo);
+            reinterpret_cast<uint4*>(s_in + kLQ), reinterpret_cast<uint32_t*>(s_in + kLX),
+            reinterpret_cast<uint32_t*>(s_in + kLR), s_lut, s_lo);
     }
 }
 

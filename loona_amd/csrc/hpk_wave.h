@@ -50,7 +50,31 @@
 #define HPK_CW_LANE_DIAG 0  // (measurement only) 2: no copy loop, 3: 16-byte pieces at 16-aligned
                             // addresses, 4: no 16-byte stores
 #endif
+#ifndef HPK_NT_STORE
+#define HPK_NT_STORE 1  // 1: the image write-back as nontemporal 16-byte stores (the output is never re-read)
+#endif
+#ifndef HPK_NT_LOAD
+#define HPK_NT_LOAD 1  // 1: the window prefetch as nontemporal 16-byte loads (each input byte is read once)
+#endif
+
 namespace hpkdec {
+
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16(uint4* p, const uint4 v) {
+    if (HPK_NT_STORE) {
+        const v4u32 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<v4u32*>(p));
+    } else {
+        *p = v;
+    }
+}
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+    if (HPK_NT_LOAD) {
+        const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    }
+    return *p;
+}
 
 template <int kWinB, int kImgB>
 struct GeoW {
@@ -66,7 +90,6 @@ struct GeoW {
     static_assert(kLdsBytes <= 163840, "LDS budget (160 KiB per CU on gfx950)");
     static_assert(kWinB % 16 == 0 && kImgB % 16 == 0 && kWinB < 65536 && kImgB < 131072, "entry packing");
     // the long-literal phase's rings and queues (hpk_long.h) over the wave areas after the fills
-    static_assert(kWaves * kWaveBytes >= 512 * (32 * 4 + HPK_LONG_OS) + 8 * 128 * 16, "long-phase LDS");
     static_assert(kWaves * kWaveBytes >= huge_lds_bytes<kBlock>(), "huge-phase LDS");
 };
 
@@ -186,20 +209,59 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         }
         __syncthreads();
         if (s_ctr[4] > s_ctr[5] / 2u) {  // block-uniform
+            // round 6: the list in LPT order (lpt_class_of, longest first) by a counting sort over the wave
+            // areas (free before the fills): the long phase takes it front to back, so the longest jobs start
+            // first; huge literals to the huge list; validated before anything is allocated
+            uint32_t* const s_cls = reinterpret_cast<uint32_t*>(smem + G::kWaveOff);  // counts, then cursors
+            if (tid < 64) s_cls[tid] = 0;
+            __syncthreads();
             bool no = false;
             for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
                 const uint32_t p0 = a.in_off[i], p1 = a.in_off[i + 1];
                 const uint32_t q0 = kCompact ? ulay(i, p0) : a.out_off[i], q1 = kCompact ? ulay(i + 1u, p1) : a.out_off[i + 1];
                 const bool ok = p0 <= p1 && p1 <= a.in_cap && q0 <= q1 && q1 <= a.out_cap &&
                                 (uint64_t)(q1 - q0) >= (uint64_t)(p1 - p0) * 8u / 5u;
-                if (ok)
-                    leave(i, p1 - p0);
-                else
+                if (!ok) {
                     no = true;
+                    continue;
+                }
+                const uint32_t nb = p1 - p0;
+                if (!(nb >= HPK_HUGE_MIN && nb < kHugeLimit)) atomicAdd(&s_cls[lpt_class_of(nb)], 1u);
             }
             if (__any(no) && lane == 0) s_ctr[6] = 1u;
             __syncthreads();
             dense = s_ctr[6] == 0u;
+            if (dense) {
+                if (tid < 64) {  // class bases
+                    const uint32_t v = tid < 32 ? s_cls[tid] : 0u;
+                    uint32_t x = v;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(x, d);
+                        if (lane >= (uint32_t)d) x += y;
+                    }
+                    if (tid < 32) s_cls[32 + tid] = x - v;
+                    if (tid == 31) s_ctr[1] = x;  // the front's count
+                }
+                __syncthreads();
+                for (uint32_t i = BA + tid; i < BB; i += G::kBlock) {
+                    const uint32_t nb = a.in_off[i + 1] - a.in_off[i];
+                    if (kCompact) a.co_off[i] = wg0 + atomicAdd(&s_ctr[9], ((nb * 8u) / 5u + 3u) & ~3u);
+                    bool huge = false;
+                    if (nb >= HPK_HUGE_MIN && nb < kHugeLimit) {
+                        const uint32_t hh = atomicAdd(&s_ctr[8], 1u);
+                        if (hh < kHugeMax) {
+                            s_huge[hh] = i;
+                            huge = true;
+                        }
+                    }
+                    // (huge literals past the huge list's room go to the list's back, LPT class 0 taken last)
+                    if (!huge)
+                        a.long_list[nb >= HPK_HUGE_MIN && nb < kHugeLimit ? BB - 1u - atomicAdd(&s_ctr[2], 1u)
+                                                                          : BA + atomicAdd(&s_cls[32 + lpt_class_of(nb)], 1u)] = i;
+                }
+                __syncthreads();
+            }
             if (!dense) {  // not all listable: the range goes through the wave fills after all
                 __syncthreads();
                 if (tid == 0) {
@@ -274,7 +336,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             pc = c;
             const uint4* g16 = reinterpret_cast<const uint4*>(a.in_base);
 #pragma unroll
-            for (int r = 0; r < R; ++r) ch[r] = g16[min((base16 >> 4) + lane + 64u * r, last16)];
+            for (int r = 0; r < R; ++r) ch[r] = ld16(g16 + min((base16 >> 4) + lane + 64u * r, last16));
         };
         // the end offsets of the slots (wave_shl:1, lane i takes lane i + 1's value; lane 63 the next
         // round's first, or slot 128's; a slot at or past the batch's last takes slot 128's)
@@ -338,7 +400,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
                 for (int r = 0; r < F; ++r) {
                     const uint32_t ci = c0 + lane + 64u * r;
                     if (ci < c1) {
-                        if ((ci << 4) >= pG0 && (ci << 4) + 16u <= pG1) g16[ci] = l16[ci - c0];
+                        if ((ci << 4) >= pG0 && (ci << 4) + 16u <= pG1) st16(g16 + ci, l16[ci - c0]);
                     }
                 }
             }
@@ -828,10 +890,15 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     if (c1 + c2) {
         static_assert(G::kWaveOff % 16 == 0, "long-phase rings");
         uint8_t* const area = smem + G::kWaveOff;
-        constexpr int kLOS = 80;  // output buffer bytes per lane (the fill kernel's default geometry)
-        long_phase<512, 8, 32, 0, G::kBlock, kLOS, 64, kTab>(a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area),
-                                                   area + 512 * 32 * 4,
-                                                   reinterpret_cast<uint4*>(area + 512 * (32 * 4 + kLOS)), s_lut, s_lo);
+        constexpr int kLB = HPK_LONG_WAVES * 64;  // the fill kernel's geometry (hpk_long.h)
+        constexpr int kLQ = kLB * (HPK_LONG_RING * 4 + HPK_LONG_OS);
+        constexpr int kLX = kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16;  // queue extra words
+        constexpr int kLR = kLX + HPK_LONG_WAVES * HPK_LONG_CLAIM * 4;   // split records
+        static_assert(kLR + HPK_LONG_WAVES * 64 * 36 <= G::kWaves * G::kWaveBytes, "long-phase LDS");
+        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, kTab>(
+            a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area), area + kLB * HPK_LONG_RING * 4,
+            reinterpret_cast<uint4*>(area + kLQ), reinterpret_cast<uint32_t*>(area + kLX),
+            reinterpret_cast<uint32_t*>(area + kLR), s_lut, s_lo);
     }
     stamp(10);
     if (kMode == 3) {

@@ -65,7 +65,8 @@ if mode == 5:  # hpk_decode_long's per-wave counters
     buf = np.zeros(256 * 16 * 16, np.uint64)
     got = L.hpk_debug_stamps(buf.ctypes.data, buf.size)
     st8 = buf[:got].reshape(-1, 16).astype(np.int64)
-    names = ["cycles", "points", "lane_steps", "stalled", "idle", "assign_cyc", "step_cyc", "ringwrite_cyc", "literals"]
+    names = ["cycles", "points", "lane_steps", "stalled", "idle_no_literal", "assign_cyc", "step_cyc", "refill_cyc", "-",
+             "idle_first_chunks", "idle_ended", "ringwrite_wait_cyc"]
     res["long_per_wave"] = {nm: {"mean": round(float(st8[:, i].mean()), 1), "max": int(st8[:, i].max()),
                                  "min": int(st8[:, i].min())} for i, nm in enumerate(names)}
 print(json.dumps(res), flush=True)
