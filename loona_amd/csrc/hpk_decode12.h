@@ -1150,16 +1150,13 @@ __global__ __launch_bounds__(kWaves * 64) void hpk_decode12(DecodeArgs a) {
         // lengths (all free once the fills are done)
         constexpr int kLB = HPK_LONG_WAVES * 64;
         constexpr int kLQ = kLB * (HPK_LONG_RING * 4 + HPK_LONG_OS);
-        constexpr int kLX = kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16;   // queue extra words
-        constexpr int kLR = kLX + HPK_LONG_WAVES * HPK_LONG_CLAIM * 4;    // split records
-        static_assert(kLR + HPK_LONG_WAVES * 64 * 36 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
+        static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= kW + kO + 12 * kQ && G::kInOff % 16 == 0 &&
                           kW % 16 == 0 && kLQ % 16 == 0 && G::kHistOff == G::kInOff + kW + kO + 12 * kQ,
                       "long-phase LDS");
         long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, 2,
                    kCompact>(
             a, BA, BB, s_ctr[6], s_ctr[7], &s_ctr[5], reinterpret_cast<uint32_t*>(s_in), s_in + kLB * HPK_LONG_RING * 4,
-            reinterpret_cast<uint4*>(s_in + kLQ), reinterpret_cast<uint32_t*>(s_in + kLX),
-            reinterpret_cast<uint32_t*>(s_in + kLR), s_lut, s_lo);
+            reinterpret_cast<uint4*>(s_in + kLQ), s_lut, s_lo);
     }
 }
 

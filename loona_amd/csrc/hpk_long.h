@@ -72,9 +72,10 @@ __device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t gb
     }
 }
 
-// LPT class of a literal listed for this phase (which takes its list front to back): its job size, half the
-// literal for one decoded as two halves (HPK_LONG_SPLIT), in 128-byte classes, 0 the longest. The dense
-// listings order their lists by it (a counting sort), so the longest jobs start first.
+// LPT class of a literal listed for this phase (which takes its list front to back): its encoded length in
+// 128-byte classes, 0 the longest. The dense listings order their lists by it (a counting sort), so the
+// longest literals start first (round 6: config 3 810 -> 635 us; the phase's length had been set by each
+// workgroup's longest literal started late, 25 % of its lane-steps idle at the end).
 __device__ __forceinline__ uint32_t lpt_class_of(uint32_t nb);
 
 // Keep a value's register live (and unchanged) up to here.
@@ -100,15 +101,8 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
                            // some lane of 64 is nearly always in its tail)
 #endif
 
-#ifndef HPK_LONG_SPLIT
-#define HPK_LONG_SPLIT 0  // round 6: literals of >= this many encoded bytes decoded as two halves (0: off; measured slower
-                          // than the LPT list order alone: config 3 930 vs 635 us, profiles/r06/split_rejected/)
-#endif
-
-#ifndef HPK_LONG_LEAD
-#define HPK_LONG_LEAD 64  // bytes the second half of a split literal walks before its split point (512 bits: a walk
-                          // started anywhere in config-3 text met the true one within 512 bits in all of 19,609
-                          // samples, within 256 bits in 99.66 %; scripts/sync_stats.py)
+#ifndef HPK_LONG_CH
+#define HPK_LONG_CH 2  // 16-byte chunks a lane loads per refill point
 #endif
 
 #ifndef HPK_LONG_OS
@@ -124,18 +118,15 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 #define HPK_LONG_BODY 1  // v28: body steps (no fit tests) while a literal has >= kBodyMin bits left
 #endif
 
-__device__ __forceinline__ uint32_t lpt_class_of(uint32_t nb) {
-    const uint32_t key = (HPK_LONG_SPLIT && nb >= (uint32_t)HPK_LONG_SPLIT) ? nb >> 1 : nb;
-    return 31u - min(key >> 7, 31u);
-}
+__device__ __forceinline__ uint32_t lpt_class_of(uint32_t nb) { return 31u - min(nb >> 7, 31u); }
 
 template <int kBlock, int kU, int kRing, int kDiag, int kBlockAll, int kOSz = HPK_LONG_OS, int kClaim = 64,
           int kTab = 2,            // kTab: the layout of s_lut (2 = LUT2, the fill kernel; 3 = LUT3, the wave kernel)
-          bool kCompact = false>   // the compacted mode: a claim takes its literals' decoded bounds from a.cursor
+          bool kCompact = false,   // the compacted mode: a claim takes its literals' decoded bounds from a.cursor
+          int kCh = HPK_LONG_CH>   // 16-byte chunks loaded per lane and refill point
 __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uint32_t bb, uint32_t c1, uint32_t c2,
                                            uint32_t* s_claim, uint32_t* s_ring, uint8_t* s_out, uint4* s_q,
-                                           uint32_t* s_qx, uint32_t* s_rec, const uint32_t* s_lut,
-                                           const uint16_t* s_lo) {
+                                           const uint32_t* s_lut, const uint16_t* s_lo) {
     constexpr uint32_t kChunk = kClaim;        // list entries per claim (at most one per lane)
     constexpr uint32_t kQ = kChunk;            // per-wave queue: a claim is made only once the lanes that
                                                // want a literal have emptied the queue, so it never holds
@@ -146,34 +137,15 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     // front, so a period starts with <= 15 bytes and adds <= 5 per step: 15 + 5 kU + 3 bytes
     // (a step's 4-byte store) must fit.
     constexpr uint32_t kOS = kOSz;
-    // (HPK_LONG_TAILPT: a tail at the refill point adds <= 6 bytes; a first half's crossing of its end <= 11:
-    // the codes starting in the < 54 bits before it)
-    static_assert(15 + 5 * kU + 3 + (HPK_LONG_SPLIT ? 11 : HPK_LONG_TAILPT ? 6 : 0) < (int)kOS, "output buffer");
-    static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16, "input ring: a power of two >= 16 dwords");
+    // (HPK_LONG_TAILPT: a tail at the refill point adds <= 6 bytes: < kBodyMin bits, codes of >= 5 bits)
+    static_assert(15 + 5 * kU + 3 + (HPK_LONG_TAILPT ? 6 : 0) < (int)kOS, "output buffer");
+    static_assert((kRing & (kRing - 1)) == 0 && kRing >= 16 && 4 * kCh + 8 <= kRing, "input ring: a power of two >= 16 dwords");
     static_assert(kBlock % 64 == 0 && kBlock <= kBlockAll, "decoding waves");
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t total = c1 + c2;
     if (total == 0) return;  // (block-uniform: nothing left to this phase)
     if (tid >= (uint32_t)kBlock) return;  // (no barrier follows)
     uint4 (*sq)[kQ] = reinterpret_cast<uint4 (*)[kQ]>(s_q);
-    // Split literals (HPK_LONG_SPLIT, round 6). The phase's length is set by each workgroup's longest
-    // literal, one lane's serial walk (config 3: ~1,240 steps against ~800 per lane on average, 25 % of the
-    // lane-steps idle at the end). A literal of >= HPK_LONG_SPLIT bytes is decoded as two halves by two
-    // lanes of the same wave: the first half (kP0) from the literal's start to its first code boundary at
-    // or after the split point s (E0); the second half (kLead) from kLeadB bytes before s with no output
-    // until its walk reaches a code boundary at or after s (S1, kP1 from there: a walk started anywhere
-    // falls into step with the true one within HPK_LONG_LEAD bytes nearly always on header text), its bytes at the provisional offset floor(8 (s - start) / 5) of the region
-    // (s - start is a multiple of 5, and the first half's codes all start before s, so its bytes fit
-    // below). When both halves are done the wave joins them: S1 == E0 -> the second half's bytes move down
-    // to follow the first's; otherwise the walk is redone from E0 (kCont, a true start) by the lane that
-    // finished last. An EOS in the second half's lead-in is a 30-bit code, not an error. Per wave: kRecs
-    // records of 8 words (o0, E0 - s8 | st0 << 16, S1 - s8, c0, c1, st1, done bits then the literal's index,
-    // P1) and one extra word per queue entry (start bit, mode, record).
-    constexpr uint32_t kNorm = 0, kP0 = 1, kLead = 2, kP1 = 3, kCont = 4;
-    constexpr uint32_t kLeadB = HPK_LONG_LEAD, kRecs = 64, kRecW = 8;
-    uint32_t* const qx = s_qx + wv * kQ;
-    uint32_t* const rec_base = s_rec + wv * kRecs * kRecW;
-    uint64_t recfree = ~0ull;  // wave-uniform: free records
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     // (whole 16-byte chunks: a load that reaches past num_records reads 0 in all its dwords)
     const __amdgpu_buffer_rsrc_t r_in = buf_rsrc(a.in_base, (in_end + 15u) & ~15u);
@@ -191,10 +163,8 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
     // next, fl the first not yet stored to global memory, lb the one at the buffer's front.
     bool act = false, live = false, pend = false, done = false;
     uint32_t idx = 0, X = 0, Eb = 0, d0 = 0, d1 = 0, d2 = 0, st = HPK_OK, q0 = 0, span = 0, h = 0;
-    uint32_t mode = kNorm, rec = 0, sbX = 0;  // (HPK_LONG_SPLIT) the lane's part of a split literal, its
-                                              // record, the split point in its X coordinates
     uint32_t o0 = 0, ob = 0, fl = 0, lb = 0;
-    u32x4 P0 = {}, P1 = {};
+    u32x4 P[kCh] = {};  // the chunks loaded at the previous refill point
     unsigned long long dg[12] = {};  // kDiag: 0 cycles, 1 points, 2 lane-steps, 3 stalled, 4 idle (no literal),
                                      // 9 waiting for a literal's first chunks, 10 ended and waiting, 11 ring-write cycles,
                                      // 5 assign cycles, 6 step cycles, 7 refill cycles, 8 literals
@@ -207,15 +177,14 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
         if (pend) {
             if (kDiag) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint32_t b = h & (kRing - 1u);
-            ring[(b + 0) * kBlock] = __builtin_bswap32(P0.x);
-            ring[(b + 1) * kBlock] = __builtin_bswap32(P0.y);
-            ring[(b + 2) * kBlock] = __builtin_bswap32(P0.z);
-            ring[(b + 3) * kBlock] = __builtin_bswap32(P0.w);
-            ring[(b + 4) * kBlock] = __builtin_bswap32(P1.x);
-            ring[(b + 5) * kBlock] = __builtin_bswap32(P1.y);
-            ring[(b + 6) * kBlock] = __builtin_bswap32(P1.z);
-            ring[(b + 7) * kBlock] = __builtin_bswap32(P1.w);
-            h += 8u;
+#pragma unroll
+            for (int c = 0; c < kCh; ++c) {
+                ring[((b + 4 * c + 0) & (kRing - 1u)) * kBlock] = __builtin_bswap32(P[c].x);
+                ring[((b + 4 * c + 1) & (kRing - 1u)) * kBlock] = __builtin_bswap32(P[c].y);
+                ring[((b + 4 * c + 2) & (kRing - 1u)) * kBlock] = __builtin_bswap32(P[c].z);
+                ring[((b + 4 * c + 3) & (kRing - 1u)) * kBlock] = __builtin_bswap32(P[c].w);
+            }
+            h += 4u * kCh;
             pend = false;
         }
         if (kDiag) {
@@ -229,69 +198,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             d1 = ring[j * kBlock];
             d2 = ring[(j + 1u) * kBlock];
             live = true;
-        }
-        // 2a. (HPK_LONG_SPLIT) halves within 54 bits (a body step's reach) of the split point, the ring holding
-        // what they read: lookups that take a table entry's second code only if it starts before the split
-        // point (a 13..30-bit code or EOS by the leading-ones table), until the walk reaches the split point
-        if (HPK_LONG_SPLIT) {
-            for (;;) {
-                const bool cr = act && live && !done && (mode == kP0 || mode == kLead) && sbX - X < 54u &&
-                                (h * 4u >= span || h >= ((sbX + 30u) >> 5) + 2u);
-                if (!__any(cr)) break;
-                bool reached = false;
-                if (cr) {
-                    const uint32_t j0 = X >> 5;
-                    const uint32_t d3 = ring[((j0 + 2u) & (kRing - 1u)) * kBlock];
-                    const uint32_t w = __builtin_amdgcn_alignbit(d0, d1, ~X);
-                    const uint32_t e = s_lut[w >> (32 - HPK_LUT_BITS)];
-                    const uint32_t nc = kTab == 3 ? HPK_L3_CODES(e) : HPK_L2_CODES(e);
-                    if (nc != 0u) {  // one or two codes of <= 12 bits: the first starts before the split point
-                        const uint32_t l0 = kTab == 3 ? HPK_L3_LEN0(e) : HPK_L2_LEN0(e);
-                        const uint32_t u = kTab == 3 ? HPK_L3_HELD(e) : HPK_L2_HELD(e);
-                        const bool two = nc == 2u && X + l0 < sbX;
-                        if (mode == kP0) {
-                            uint8_t* const p = obuf + (ob - lb);
-                            p[0] = (uint8_t)e;
-                            p[1] = (uint8_t)(e >> 16);
-                            ob += two ? 2u : 1u;
-                        }
-                        const uint32_t xn = X + (two ? u : l0);
-                        const bool cross = (xn ^ X) > 31u;
-                        d0 = cross ? d1 : d0;
-                        d1 = cross ? d2 : d1;
-                        d2 = cross ? d3 : d2;
-                        X = xn;
-                        reached = X >= sbX;
-                    } else {
-                        uint32_t sy, len;
-                        bool eos;
-                        lo_decode(w, s_lo, sy, len, eos);
-                        if (mode == kP0 && eos) {  // the first half's EOS is the literal's (huffman.rs:112-116)
-                            st = HPK_EOS_IN_STRING;
-                            done = true;
-                        } else {  // (an EOS in the lead-in: a 30-bit code, lo_decode's len)
-                            if (mode == kP0) {
-                                obuf[ob - lb] = (uint8_t)sy;
-                                ob += 1u;
-                            }
-                            X += len;
-                            const uint32_t j = X >> 5;
-                            d0 = ring[((j - 1u) & (kRing - 1u)) * kBlock];
-                            d1 = ring[(j & (kRing - 1u)) * kBlock];
-                            d2 = ring[((j + 1u) & (kRing - 1u)) * kBlock];
-                            reached = X >= sbX;
-                        }
-                    }
-                }
-                if (reached) {
-                    if (mode == kP0) {
-                        done = true;  // E0 recorded when it is finished (4)
-                    } else {          // the second half is at S1: its output starts here
-                        rec_base[rec * kRecW + 2] = X - sbX;
-                        mode = kP1;
-                    }
-                }
-            }
         }
         // 2b. (HPK_LONG_TAILPT) lanes whose literal has fewer than kBodyMin bits left, all of its chunks in
         // the ring: checked steps (lit12_step's) until the walk ends; the literal is finished in 4 below
@@ -400,12 +306,9 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 lb = fl;
             }
         }
-        // 4. a literal that ended in the last steps: padding check, last bytes, length, status (a half of a
-        // split literal: its record instead; the lane that completes the record joins it, 4b)
-        bool jown = false;
+        // 4. a literal that ended in the last steps: padding check, last bytes, length, status
         if (done) {
-            if (st == HPK_OK && mode != kP0 && mode != kLead)
-                st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
+            if (st == HPK_OK) st = residual_status(Eb - X, __builtin_amdgcn_alignbit(d0, d1, ~X));
             if (ob > fl) {  // [fl, ob) lies in one group, at the buffer's front
                 const uint32_t gb = fl & ~15u;
                 ta = gb;
@@ -420,99 +323,11 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             sv = st;
             ia = idx * 4u;
             ja = idx;
-            if (!HPK_LONG_SPLIT || mode == kNorm || mode == kCont) {
-                __builtin_amdgcn_raw_buffer_store_b32(lv, r_len, ia, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sv, r_st, ja, 0, 0);
-            } else {
-                uint32_t* const R = rec_base + rec * kRecW;
-                uint32_t bit;
-                if (mode == kP0) {
-                    R[1] = ((X - sbX) & 0xFFFFu) | (sv << 16);  // E0 (meaningless after an EOS) and the first half's status
-                    R[3] = lv;
-                    bit = 1u;
-                } else {  // kP1 (a kLead cannot end before its lead-in does; if it did, R[2] has no S1)
-                    R[4] = lv;
-                    R[5] = sv;
-                    bit = 2u;
-                }
-                jown = (atomicOr(&R[6], bit) | bit) == 3u;
-            }
+            __builtin_amdgcn_raw_buffer_store_b32(lv, r_len, ia, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sv, r_st, ja, 0, 0);
             act = false;
             live = false;
             done = false;
-        }
-        // 4b. (HPK_LONG_SPLIT) joins, one record at a time by the whole wave: halves that met (S1 == E0) have
-        // the second half's bytes moved down behind the first's (16-byte pieces, ascending: a piece's
-        // destination never reaches a later piece's source); halves that did not meet have the walk redone
-        // from E0 by the lane that completed the record (kCont: a true start at a bit offset, its bytes
-        // straight after c0); a first half's EOS is the literal's status at once
-        if (HPK_LONG_SPLIT) {
-            bool fr = mode == kCont && !act && rec != 0xFFFFFFFFu;  // a continuation finished in 4
-            while (__any(jown)) {
-                const uint32_t L = (uint32_t)__builtin_ctzll(__ballot(jown));
-                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)L);
-                const uint32_t* const R = rec_base + r * kRecW;
-                const uint32_t ro0 = R[0], e0 = R[1] & 0xFFFFu, s1 = R[2], c0 = R[3];
-                const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)L);
-                bool freed = true;
-                uint32_t olen = c0, ost = R[1] >> 16;
-                if (ost == HPK_OK && e0 == s1) {  // the second half's bytes moved down behind the first's
-                    const uint32_t c1 = R[4], p1 = R[7];
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the halves' stores are done
-                    const uint32_t dst = ro0 + c0;
-                    for (uint32_t off = 0; off < c1; off += 1024u) {
-                        // (every lane's 16-byte piece is read before any is stored; a whole piece's store ends
-                        // at or below the next lane's destination, below every later source byte, so the
-                        // last lane's bytes, copied after, are still in place)
-                        const uint32_t j = off + lane * 16u;
-                        const bool whole = j + 16u <= c1;
-                        if (whole) {
-                            const u32x4u v = *reinterpret_cast<const u32x4u*>(a.out_base + p1 + j);
-                            *reinterpret_cast<u32x4u*>(a.out_base + dst + j) = v;
-                        }
-                        if (!whole)  // (after the whole pieces: see above)
-                            for (uint32_t k = j; k < c1; ++k) a.out_base[dst + k] = a.out_base[p1 + k];
-                    }
-                    olen = c0 + c1;
-                    ost = R[5];
-                } else if (ost == HPK_OK) {  // the halves did not meet: lane L redoes the walk from E0
-                    freed = false;
-                    if (lane == L) {
-                        const uint32_t sbyte = q0 * 16u + ((sbX - 31u) >> 3);  // (abs, incl. in_mis)
-                        const uint32_t pend_b = q0 * 16u + ((Eb - 31u) >> 3);
-                        const uint32_t p0 = sbyte + (e0 >> 3);
-                        act = true;
-                        live = false;
-                        mode = kCont;
-                        q0 = p0 >> 4;
-                        span = pend_b - (q0 << 4);
-                        X = (p0 & 15u) * 8u + (e0 & 7u) + 31u;
-                        Eb = (pend_b - (q0 << 4)) * 8u + 31u;
-                        h = 0;
-                        st = HPK_OK;
-                        o0 = ro0;
-                        ob = ro0 + c0;
-                        fl = ob;
-                        lb = ob & ~15u;
-                    }
-                }
-                if (freed) {
-                    if (lane == 0) {
-                        a.out_len[li] = olen;
-                        a.status[li] = (uint8_t)ost;
-                    }
-                    recfree |= 1ull << r;
-                }
-                if (lane == L) jown = false;
-            }
-            while (__any(fr)) {  // continuations done: their records free
-                const uint32_t L = (uint32_t)__builtin_ctzll(__ballot(fr));
-                recfree |= 1ull << (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)L);
-                if (lane == L) {
-                    fr = false;
-                    rec = 0xFFFFFFFFu;
-                }
-            }
         }
         if (kDiag) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -528,7 +343,6 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
             if (want && qh + rank < qt) {
                 const uint4 te = sq[wv][(qh + rank) % kQ];
-                const uint32_t x = HPK_LONG_SPLIT ? qx[(qh + rank) % kQ] : 0u;
                 idx = te.x;
                 act = true;
                 live = false;
@@ -543,23 +357,14 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 ob = o0;
                 fl = o0;
                 lb = o0 & ~15u;
-                mode = (x >> 3) & 7u;
-                rec = x >> 6;
-                // the split point in the lane's X: kLeadB bytes in (kLead), the literal's halfway point (kP0)
-                sbX = X + (mode == kP0 ? ((te.z - te.y) / 10u) * 5u : kLeadB) * 8u;
             }
             const uint32_t need = (uint32_t)__popcll(wm);
             const bool enough = need <= qt - qh;
             qh += min(need, qt - qh);
             if (enough || !more || claims == 2) break;  // (at most two claims per refill point)
-            // claim the next entries of this workgroup's list (an LDS counter): as many as the queue has room for,
-            // two slots each (a literal of >= HPK_LONG_SPLIT bytes is queued as its two halves, kP0 then kLead,
-            // with a record, while records last: taken by the next lanes that want work, so the halves of the
-            // list's first (longest) literals start together)
-            const uint32_t room = HPK_LONG_SPLIT ? (kQ - (qt - qh)) / 2u : kQ - (qt - qh);
-            if (room == 0u) break;
+            // claim the next 64 entries of this workgroup's list (an LDS counter)
             uint32_t rr = 0;
-            if (lane == 0) rr = atomicAdd(s_claim, room);
+            if (lane == 0) rr = atomicAdd(s_claim, kChunk);
             const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rr, 0);
             if (r >= total) {
                 more = false;
@@ -567,7 +372,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             }
             // entries r + lane: [0, c1) from the front of the range, then from the back
             const uint32_t e = r + lane;
-            const bool ok = lane < room && e < total;
+            const bool ok = lane < kChunk && e < total;
             const uint32_t lpos = ok ? (e < c1 ? ba + e : bb - 1u - (e - c1)) : ba;
             const uint32_t i0 = a.long_list[lpos];  // (a load either way: see the note below)
             const uint32_t i = ok ? i0 : 0u;
@@ -591,44 +396,10 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             } else {
                 li = make_uint4(i, a.in_off[i], a.in_off[i + 1], a.lit_out[i]);
             }
-            bool sp = false;
-            uint32_t srec = 0;
-            if (HPK_LONG_SPLIT) {
-                uint64_t cm = __ballot(ok && li.z - li.y >= (uint32_t)HPK_LONG_SPLIT);
-                while (cm && recfree) {
-                    const uint32_t L = (uint32_t)__builtin_ctzll(cm);
-                    const uint32_t rf = (uint32_t)__builtin_ctzll(recfree);
-                    recfree &= recfree - 1ull;
-                    cm &= cm - 1ull;
-                    if (lane == L) {
-                        srec = rf;
-                        sp = true;
-                    }
-                }
-            }
-            const uint32_t k = ok ? (sp ? 2u : 1u) : 0u;
-            uint32_t inc = k;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(inc, d);
-                if (lane >= (uint32_t)d) inc += y;
-            }
-            const uint32_t slot = qt + inc - k;
-            if (ok) {
-                sq[wv][slot % kQ] = li;
-                if (HPK_LONG_SPLIT) qx[slot % kQ] = sp ? (kP0 << 3) | (srec << 6) : 0u;
-            }
-            if (sp) {  // the second half, and the record
-                const uint32_t hb = ((li.z - li.y) / 10u) * 5u;  // a multiple of 5 bytes in (>= kLeadB)
-                sq[wv][(slot + 1u) % kQ] = make_uint4(li.x, li.y + hb - kLeadB, li.z, li.w + (hb / 5u) * 8u);
-                qx[(slot + 1u) % kQ] = (kLead << 3) | (srec << 6);
-                uint32_t* const R = rec_base + srec * kRecW;
-                R[0] = li.w + a.out_mis;
-                R[2] = 0xFFFFFFFFu;
-                R[6] = 0u;
-                R[7] = li.w + a.out_mis + (hb / 5u) * 8u;
-            }
-            qt += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            const uint64_t lm = __ballot(ok);
+            const uint32_t lr = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+            if (ok) sq[wv][(qt + lr) % kQ] = li;
+            qt += (uint32_t)__popcll(lm);
         }
         if (kDiag) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -636,10 +407,11 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
             dtp = t;
         }
         if (!__any(act)) break;  // no literal left for this wave
-        // 6. the next two chunks, while the ring has room for them past the window's first dword
-        if (act && h * 4u < span && h + 8u + 1u <= kRing + (X >> 5)) {
-            P0 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u, 0, 0);
-            P1 = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u + 16u, 0, 0);
+        // 6. the next kCh chunks, while the ring has room for them past the window's first dword
+        if (act && h * 4u < span && h + 4u * kCh + 1u <= kRing + (X >> 5)) {
+#pragma unroll
+            for (int c = 0; c < kCh; ++c)
+                P[c] = __builtin_amdgcn_raw_buffer_load_b128(r_in, (q0 + (h >> 2)) * 16u + 16u * c, 0, 0);
             pend = true;
         }
         // ---- kU steps while the input ring holds what a step can reach: a step advances < 2 dwords
@@ -650,8 +422,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                                 : h * 4u >= span ? (uint32_t)kU
                                 : x5 + 4u <= h ? min((uint32_t)kU, ((h - x5 - 4u) >> 1) + 1u) : 0u;
         for (int s = 0; s < kU; ++s) {
-            const bool go = (uint32_t)s < budget && !done && (!HPK_LONG_TAILPT || Eb - X >= kBodyMin) &&
-                            (!HPK_LONG_SPLIT || !(mode == kP0 || mode == kLead) || sbX - X >= 54u);
+            const bool go = (uint32_t)s < budget && !done && (!HPK_LONG_TAILPT || Eb - X >= kBodyMin);
             if (kDiag) {
                 dg[2] += (unsigned long long)__popcll(__ballot(go));
                 dg[3] += (unsigned long long)__popcll(__ballot(act && live && !done && !go));
@@ -703,7 +474,7 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 p[1] = (uint8_t)(e1 >> 16);
                 p[g1] = (uint8_t)e2;
                 p[g1 + 1] = (uint8_t)(e2 >> 16);
-                ob += HPK_LONG_SPLIT && mode == kLead ? 0u : g1 + g2;  // (the lead-in: no output)
+                ob += g1 + g2;
             }
             const uint32_t xn = X + u1 + u2;
             const bool cross = (xn ^ X) > 31u;
@@ -719,12 +490,12 @@ __device__ __forceinline__ void long_phase(const DecodeArgs& a, uint32_t ba, uin
                 if (len > Eb - X) {  // nothing fits in the > 12 bits left: huffman.rs:128-134
                     st = HPK_PADDING_TOO_LARGE;
                     prog = false;
-                } else if (eos && !(HPK_LONG_SPLIT && mode == kLead)) {  // huffman.rs:112-116
+                } else if (eos) {  // huffman.rs:112-116
                     st = HPK_EOS_IN_STRING;
                     prog = false;
-                } else {  // (an EOS in a lead-in: a 30-bit code)
+                } else {
                     obuf[ob - lb] = (uint8_t)sy;
-                    ob += HPK_LONG_SPLIT && mode == kLead ? 0u : 1u;
+                    ob += 1u;
                     const uint32_t xp = X + len;  // (len <= 30: crosses at most one dword)
                     // the window re-read from the ring (a select from d3 or a fourth dword read beside
                     // the lookup instead: config 3 832-836 vs 817-822 us)

@@ -892,13 +892,10 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         uint8_t* const area = smem + G::kWaveOff;
         constexpr int kLB = HPK_LONG_WAVES * 64;  // the fill kernel's geometry (hpk_long.h)
         constexpr int kLQ = kLB * (HPK_LONG_RING * 4 + HPK_LONG_OS);
-        constexpr int kLX = kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16;  // queue extra words
-        constexpr int kLR = kLX + HPK_LONG_WAVES * HPK_LONG_CLAIM * 4;   // split records
-        static_assert(kLR + HPK_LONG_WAVES * 64 * 36 <= G::kWaves * G::kWaveBytes, "long-phase LDS");
+        static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= G::kWaves * G::kWaveBytes, "long-phase LDS");
         long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, kTab>(
             a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area), area + kLB * HPK_LONG_RING * 4,
-            reinterpret_cast<uint4*>(area + kLQ), reinterpret_cast<uint32_t*>(area + kLX),
-            reinterpret_cast<uint32_t*>(area + kLR), s_lut, s_lo);
+            reinterpret_cast<uint4*>(area + kLQ), s_lut, s_lo);
     }
     stamp(10);
     if (kMode == 3) {
