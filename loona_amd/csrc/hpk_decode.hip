@@ -47,10 +47,11 @@ using Geo = Geo12<kWaves, kW, kO, kQ>;
 // ones keep the workgroup-fill kernel) unless the context says otherwise (hpk_ctx_set_decode_kernel)
 constexpr int kWaveWin = 3072, kWaveImg = 5888;
 #ifndef HPK_WAVE_MIN
-#define HPK_WAVE_MIN 4000000u
+#define HPK_WAVE_MIN 0u  // (round 6: the wave kernel for every batch; it had been 4M: config 2 40.3-40.8 vs 47.1-47.3 us
+                         // for the workgroup-fill kernel, 1k-literal synchronous calls 21.5 vs 24.4 us)
 #endif
 #ifndef HPK_WAVE_GUIDED
-#define HPK_WAVE_GUIDED 1  // chunks claimed by the waves (guided self-scheduling) vs a static 1/16 each
+#define HPK_WAVE_GUIDED 1  // chunks claimed by the waves (1: guided self-scheduling, 2: fixed HPK_WAVE_CHUNK) vs a static 1/16 each (0)
 #endif
 #ifndef HPK_WAVE_RANK
 #define HPK_WAVE_RANK 0  // longest-first order: 0 LDS counting sort (32 classes), 1/2 ballots (16/32 classes)
@@ -59,6 +60,16 @@ constexpr int kWaveWin = 3072, kWaveImg = 5888;
 #define HPK_WAVE_CHUNK 224u  // least literals per chunk claim
 #endif
 #define WAVE_KERNEL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, HPK_WAVE_CHUNK, HPK_WAVE_GUIDED, HPK_WAVE_RANK>
+// (round 6) batches below HPK_WAVE_GUIDED_MIN literals hand their workgroups' ranges out in fixed chunks of
+// about one fill (config 2 with 104-literal chunks: 43.7-43.9 us against 51.1 guided, 44.1-45.0 static, 46.9
+// for the workgroup-fill kernel; with the overlapped start, hpk_wave.h, and 96-literal chunks 40.3-40.6)
+#ifndef HPK_WAVE_GUIDED_MIN
+#define HPK_WAVE_GUIDED_MIN 4000000u
+#endif
+#ifndef HPK_WAVE_SMALL_CHUNK
+#define HPK_WAVE_SMALL_CHUNK 96u  // (config 2: 88 43.1-43.5, 92 40.5-41.0, 96 40.3-40.6, 100 42.4-43.3, 104 43.3-43.9 us)
+#endif
+#define WAVE_KERNEL_SMALL(m) hpk_decode_wave<m, kWaveWin, kWaveImg, HPK_WAVE_SMALL_CHUNK, 2, HPK_WAVE_RANK>
 #define DEC_KERNEL(m) hpk_decode12<m, kWaves, kW, kO, kQ, kRefillN>
 
 #ifdef HPK_DIAG
@@ -401,7 +412,9 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
             hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);
     }
 #else
-    if (wave)
+    if (wave && b.n < HPK_WAVE_GUIDED_MIN)
+        hipLaunchKernelGGL(WAVE_KERNEL_SMALL(0), grid, block, 0, c->stream, a);
+    else if (wave)
         hipLaunchKernelGGL(WAVE_KERNEL(0), grid, block, 0, c->stream, a);
     else
         hipLaunchKernelGGL(DEC_KERNEL(0), grid, block, 0, c->stream, a);

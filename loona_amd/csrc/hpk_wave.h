@@ -119,7 +119,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 // gathered into it (compact_fill), every listed literal takes its 4-rounded bound there when it is
 // listed (co_off). No device-wide cursor: one atomic per fill on one word would be ~290k per 32M-literal
 // launch, against the ~88 per us one word takes (MI355X_MICROARCH.md, dequeue).
-template <int kMode, int kWinB, int kImgB, uint32_t kChunk, bool kGuided, int kRank, bool kCompact = false>
+template <int kMode, int kWinB, int kImgB, uint32_t kChunk, int kGuided, int kRank, bool kCompact = false>
 __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     using G = GeoW<kWinB, kImgB>;
     constexpr int kStore = kMode == 2 ? kNoStore : kPred;
@@ -149,16 +149,35 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     uint32_t* s_ctr = reinterpret_cast<uint32_t*>(smem + G::kCtrOff);
     uint32_t* s_huge = s_ctr + 16;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
-        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
     constexpr int kTab = HPK_LUT3 && HPK_BODY ? 3 : 2;  // the table layout of the fills and the phases after them
-    for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
-        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
-    if (tid < 16) s_ctr[tid] = 0;
-    if (kMode == 3)
-        for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
     const uint32_t BA = (uint32_t)((uint64_t)a.n * blockIdx.x / gridDim.x);
     const uint32_t BB = (uint32_t)((uint64_t)a.n * (blockIdx.x + 1) / gridDim.x);
+    // (round 6) The start's memory round trips overlapped: every wave's first chunk is fixed here (wave wv's
+    // c0 literals from BA + wv c0; the static split: its 1/16), and its first literal's offsets, the dense
+    // check's offsets and the tables are loaded together (they had been four dependent round trips: tables,
+    // the dense check, the first claim's offsets, then the first fill's). Config 2: see DESIGN.md §4.0.
+    static_assert(G::kBlock == 1024, "the dense check's two offsets rounds");
+    const uint32_t c0 = kGuided == 2 ? kChunk : max(kChunk, (BB - BA) / 32u);
+    const uint32_t cur0 = kGuided == 0 ? BA + (uint32_t)((uint64_t)(BB - BA) * wv / G::kWaves) : min(BA + wv * c0, BB);
+    const uint32_t ce0 =
+        kGuided == 0 ? BA + (uint32_t)((uint64_t)(BB - BA) * (wv + 1) / G::kWaves) : min(cur0 + c0, BB);
+    const uint32_t gin0 = a.in_off[cur0];
+    const uint32_t gout0 = kCompact ? 0u : a.out_off[cur0];
+    const uint32_t kd = min(BB - BA, 2048u);  // the dense check's literals: the range's first 2048
+    uint32_t dv0[2], dv1[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t tt = BA + min(tid + (uint32_t)G::kBlock * r, kd ? kd - 1u : 0u);
+        dv0[r] = a.in_off[tt];
+        dv1[r] = a.in_off[tt + 1u];
+    }
+    for (uint32_t t = tid; t < kLoBytes / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lo)[t] = reinterpret_cast<const uint4*>(a.lo)[t];
+    for (uint32_t t = tid; t < HPK_LUT_SIZE * 4 / 16; t += G::kBlock)
+        reinterpret_cast<uint4*>(s_lut)[t] = reinterpret_cast<const uint4*>(kTab == 3 ? a.lut3 : a.lut2)[t];
+    if (tid < 16) s_ctr[tid] = tid == 7 && kGuided ? min(G::kWaves * c0, BB - BA) : 0u;  // [7]: the first chunks
+    if (kMode == 3)
+        for (uint32_t t = tid; t < (uint32_t)G::kWaves * 12u; t += G::kBlock) s_dg[t] = 0;
     const uint32_t in_end = min(a.in_off[a.n], a.in_cap) + a.in_mis;
     const uint32_t last16 = in_end ? (in_end - 1) >> 4 : 0;  // last 16-B chunk holding a batch byte
     // (kCompact, v34) the bound layout is U(i) = floor(8 (in_off[i] - in_off[0]) / 5) + 4 i, made here
@@ -191,12 +210,14 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
     // ---- a range whose first literals hold mostly long-literal bytes (config 3) is listed whole ----
     bool dense = false;
     {
-        const uint32_t k = min(BB - BA, 2048u);
         uint32_t dlb = 0, dtb = 0;
-        for (uint32_t t = tid; t < k; t += G::kBlock) {
-            const uint32_t nb = min(a.in_off[BA + t + 1] - a.in_off[BA + t], 1u << 20);  // (bad offsets: bounded)
-            dtb += nb;
-            dlb += nb >= a.long_min ? nb : 0u;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (tid + (uint32_t)G::kBlock * r < kd) {
+                const uint32_t nb = min(dv1[r] - dv0[r], 1u << 20);  // (bad offsets: bounded)
+                dtb += nb;
+                dlb += nb >= a.long_min ? nb : 0u;
+            }
         }
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
@@ -308,7 +329,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             if (lane == 0) {
                 const uint32_t seen = *(volatile HPK_LDS_AS uint32_t*)(&s_ctr[7]);
                 const uint32_t left = BB - BA > seen ? BB - BA - seen : 0u;
-                const uint32_t want = max(kChunk, left / 32u);
+                const uint32_t want = kGuided == 2 ? kChunk : max(kChunk, left / 32u);  // (2: fixed chunks)
                 c = atomicAdd(&s_ctr[7], want);
                 c = c < BB - BA ? c : BB - BA;
                 ce = BA + min(c + want, BB - BA);  // (lane 0's; broadcast below)
@@ -361,13 +382,13 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         // A wave holds one chunk at a time and claims the next when its current one ends (its first
         // offsets are then loaded under the fill's setup): claimed a chunk ahead, the range's last
         // chunks were held by a few waves while the workgroup's others waited (5 % of a wave's time)
-        uint32_t cur, ce;
-        claim(cur, ce);
+        uint32_t cur = cur0, ce = ce0;  // the first chunk (above)
+        given = true;
         uint32_t gin = 0, gout = 0;
         uint32_t sens[4] = {0u, 1u, 2u, 3u};  // diagnostic modes 6 / 7 only
         if (cur < ce) {
-            gin = a.in_off[cur] + a.in_mis;
-            gout = oof(cur) + a.out_mis;
+            gin = gin0 + a.in_mis;
+            gout = (kCompact ? ulay(cur, gin0) : gout0) + a.out_mis;
             prefetch(cur, ce, gin & ~15u);
         }
         // the previous fill, not yet written back: literals [pcur, pcur + pk), output [pG0, pG1), and
