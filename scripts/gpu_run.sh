@@ -18,7 +18,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-run}; mkdir -p $OUT
 WLS=${WLS:-config5}
 LIBS=${LIBS:-libhpk.so}
-kernel_of() { case $1 in config5|c2_4m) echo hpk_decode_wave;; config3*) echo hpk_decode12;; *) echo hpk_decode12;; esac; }
+kernel_of() { echo ${DECODE_KERNEL_NAME:-hpk_decode_wave}; }  # (round 6: the wave kernel decodes every batch)
 lits_of() { case $1 in config5) echo 32000000;; c2_4m) echo 4000000;; *) echo 1000000;; esac; }
 for step in ${STEPS:-test}; do
   case $step in
