@@ -104,7 +104,8 @@ __global__ __launch_bounds__(ENC_BLOCK) void hpk_encode_kernel(EncodeArgs a) {
 // Geometry: kEB threads per workgroup, kEO bytes of LDS output image, kEQ literals per tile. The
 // product runs two workgroups of 512 threads per CU (16 KiB input tiles, 56 KiB images), so one
 // workgroup's global-memory waits overlap the other's LDS work; 1024 / 112 KiB / 2048 (one per CU)
-// stays for comparison (HPK_ENCODE_CFG=1; 2 and 3: 16 bytes per thread).
+// stays for comparison (HPK_ENCODE_CFG=1; v5 dropped the 16-bytes-per-thread geometries: the start
+// map has one word per thread).
 
 // Pass 2's phantom runs (bytes a thread holds but does not own: before the tile's first literal,
 // after its last) go to kEPh dwords past the image: a run covers at most 32 bytes of 30-bit codes
@@ -120,11 +121,14 @@ struct EncLds {
     uint2 tab[256];              // (code, length)
     uint32_t code1[256];         // serial path: codes
     uint8_t len1[256];           // serial path: lengths
-    uint32_t wf[16], wv[16];     // per-wave scan totals
+    uint32_t wf[16], wv[16], wl[16];  // per-wave scan totals
+    uint32_t smap[kEB + 1];      // bit j of word h: input byte 32h + j starts a (non-empty) literal of the tile
+    uint32_t slast[kEB + 1];     // 1 + the last (non-empty) literal starting in word h's bytes, 0 if none
     uint32_t live[(kEO / 16 + 31) / 32];  // image chunks holding output bytes (the rest is slack)
-    uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen
+    uint32_t ctr[4];             // [0] literals in the tile, [1] bad offsets seen, [2] a literal of the tile
+                                 // has less room than 30 bits per input byte (pass 2 takes the checked path)
     uint32_t split[2 * hpksplit::kMaxRounds];  // split_by_bytes's counters
-    unsigned long long prof[kP ? 16 : 1][10];   // diagnostic build (kProf): per-wave phase cycles
+    unsigned long long prof[kP ? kEB / 64 : 1][12];  // diagnostic build (kProf): per-wave phase cycles
 };
 
 
@@ -142,10 +146,50 @@ __device__ __forceinline__ void img_or(uint32_t* img, uint32_t q, uint32_t c, ui
 }
 
 
-template <int kEB, int kEO, int kEQ, int kEBytes = 32, int kProf = 0>  // kEBytes: input bytes per thread per tile (16 or 32)
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_e(uint32_t x) {  // out-of-range lanes read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, 0xF, 0xF, false);
+}
+
+template <int kCtrl>
+__device__ __forceinline__ void seg_step(uint32_t& f, uint32_t& v, uint32_t& L) {
+    const uint32_t pf = dpp_e<kCtrl>(f), pv = dpp_e<kCtrl>(v), pl = dpp_e<kCtrl>(L);
+    v = f ? v : v + pv;
+    f |= pf;
+    L = max(L, pl);
+}
+
+// Segmented inclusive scan over the wave's 64 lanes of (f, v) under (f0, v0) . (f1, v1) = (f0 | f1,
+// f1 ? v1 : v0 + v1) (f: a literal starts in the lane's bytes, v: code bits since the last start), with
+// an inclusive max of L beside it: DPP row shifts within rows of 16 lanes, then the rows' totals by
+// readlane (v5: it replaced 12 dependent ds_bpermute shuffles).
+__device__ __forceinline__ void wave_seg_scan(uint32_t& f, uint32_t& v, uint32_t& L, uint32_t lane) {
+    seg_step<0x111>(f, v, L);  // row_shr:1
+    seg_step<0x112>(f, v, L);  // row_shr:2
+    seg_step<0x114>(f, v, L);  // row_shr:4
+    seg_step<0x118>(f, v, L);  // row_shr:8
+    const uint32_t f0 = __builtin_amdgcn_readlane((int)f, 15), v0 = __builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t f1 = __builtin_amdgcn_readlane((int)f, 31), v1 = __builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t f2 = __builtin_amdgcn_readlane((int)f, 47), v2 = __builtin_amdgcn_readlane((int)v, 47);
+    const uint32_t l0 = __builtin_amdgcn_readlane((int)L, 15), l1 = __builtin_amdgcn_readlane((int)L, 31);
+    const uint32_t l2 = __builtin_amdgcn_readlane((int)L, 47);
+    // the carry into rows 1, 2, 3: row 0, rows 0-1, rows 0-2
+    const uint32_t c1f = f0, c1v = v0;
+    const uint32_t c2f = f0 | f1, c2v = f1 ? v1 : v0 + v1;
+    const uint32_t c3f = c2f | f2, c3v = f2 ? v2 : c2v + v2;
+    const uint32_t row = lane >> 4;
+    const uint32_t cf = row == 0 ? 0u : row == 1 ? c1f : row == 2 ? c2f : c3f;
+    const uint32_t cv = row == 0 ? 0u : row == 1 ? c1v : row == 2 ? c2v : c3v;
+    const uint32_t cl = row == 0 ? 0u : row == 1 ? l0 : row == 2 ? max(l0, l1) : max(max(l0, l1), l2);
+    v = f ? v : v + cv;
+    f |= cf;
+    L = max(L, cl);
+}
+
+template <int kEB, int kEO, int kEQ, int kEBytes = 32, int kProf = 0>  // kEBytes: input bytes per thread per tile
 // (at least 4 waves per SIMD: two 512-thread workgroups per CU fit only under 128 VGPRs)
 __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
-    static_assert(kEBytes == 16 || kEBytes == 32, "bytes per thread");
+    static_assert(kEBytes == 32, "bytes per thread: one start-map word per thread");
     constexpr int kCh = kEBytes / 16;  // 16-byte chunks per thread
     constexpr int kETile = kEB * kEBytes;  // input bytes per tile
     constexpr int kEMeta = kEQ / kEB;      // offset rounds per thread
@@ -154,7 +198,7 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
     __shared__ __attribute__((aligned(16))) EncLds<kEB, kEO, kEQ, kProf> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     uint64_t tprev = kProf ? clock64() : 0;
-    if (kProf && tid < 160) (&S.prof[0][0])[tid] = 0;
+    if (kProf && tid < (kEB / 64) * 12) (&S.prof[0][0])[tid] = 0;
     if (tid < 256) {
         const uint32_t c = a.codes[tid], l = a.codes[257 + tid];
         S.tab[tid] = make_uint2(c, l);
@@ -199,17 +243,27 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
     while (cur < BB) {  // block-uniform
         const uint32_t cntl = min((uint32_t)kEQ, BB - cur);
         const uint32_t base16 = gin & ~15u, ob16 = gout & ~15u;
+        EPROF(7);
         lds_barrier_e();  // the previous tile's image is out
+        EPROF(11);
         if (tid == 0) {
             S.ctr[0] = 0;
             S.ctr[1] = 0;
+            S.ctr[2] = 0;
         }
         for (uint32_t w = tid; w < (uint32_t)((kEO / 16 + 31) / 32); w += kEB) S.live[w] = 0;
-        lds_barrier_e();
+        for (uint32_t w = tid; w <= (uint32_t)kEB; w += kEB) {
+            S.smap[w] = 0;
+            S.slast[w] = 0;
+        }
         EPROF(0);
-        // which literals fit (a prefix: offsets are non-decreasing)
+        lds_barrier_e();
+        EPROF(11);
+        // which literals fit (a prefix: offsets are non-decreasing); each fitting non-empty literal marks
+        // its first byte in the start map and its index in its word's slast
         uint32_t kw = 0;
         bool bad = false;  // a literal of the tile's range with decreasing offsets or offsets past a capacity
+        bool tight = false;  // a fitting literal with less room than 30 bits per input byte
 #pragma unroll
         for (int r = 0; r < kEMeta; ++r) {
             const uint32_t t = tid + (uint32_t)kEB * r;
@@ -228,13 +282,22 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
                 S.ioff[t + 1] = i1 - base16;  // (the same value literal t + 1 writes)
                 S.ooff[t + 1] = o1 - ob16;
                 S.bits[t] = 0;
+                if (i1 > i0) {
+                    const uint32_t x = i0 - base16;
+                    atomicOr(&S.smap[x >> 5], 1u << (x & 31u));
+                    atomicMax(&S.slast[x >> 5], t + 1u);
+                }
+                tight |= (o1 - o0) * 8u < 30u * (i1 - i0);
             }
             kw += (uint32_t)__popcll(__ballot(fits));
         }
         if (lane == 0 && kw) atomicAdd(&S.ctr[0], kw);
         if (__any(bad) && lane == 0) S.ctr[1] = 1u;
+        if (__any(tight) && lane == 0) S.ctr[2] = 1u;
         const uint4 chc0 = ch[0], chc1 = ch[1];
+        EPROF(1);
         lds_barrier_e();
+        EPROF(11);
         if (S.ctr[1]) {  // bad offsets (block-uniform): the range's remaining literals are void
             for (uint32_t i = cur + tid; i < BB; i += kEB) {
                 a.out_len[i] = 0;
@@ -261,48 +324,27 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
         const uint32_t gin_n = S.ioff[k] + base16, gout_n = S.ooff[k] + ob16;
         if (cur_n < BB) prefetch(cur_n, gin_n & ~15u);
         const uint32_t xb = S.ioff[0], xe = S.ioff[k];  // the tile's input bytes [xb, xe)
-        // this thread's bytes [x0, x1) and the literal holding x0
+        const bool tile_safe = S.ctr[2] == 0u;  // every literal has room for 30 bits per byte (the longest code)
+        // this thread's bytes [x0, x1); its word of the start map gives the literal starts among them
+        // (v5: it replaced a binary search of ioff and a walk over the literals the thread touches)
         const uint32_t x0 = max(tid * (uint32_t)kEBytes, xb), x1 = min(tid * (uint32_t)kEBytes + kEBytes, xe);
         const bool any = x0 < x1;
-        uint32_t li = 0;
-        if (any) {  // largest li < k with ioff[li] <= x0 (a non-empty literal)
-            uint32_t lo = 0, hi = k - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (S.ioff[mid] <= x0)
-                    lo = mid;
-                else
-                    hi = mid - 1;
-            }
-            li = lo;
-        }
-        const bool f0 = any && S.ioff[li] == x0;  // the thread's first byte starts a literal
+        const uint32_t xt = tid * (uint32_t)kEBytes;
+        const uint32_t sm = S.smap[tid], snext = S.smap[tid + 1], sl = S.slast[tid];
         // the thread's bytes by constant index (the loops below are unrolled: no register array
         // indexed at run time, which the compiler would put in scratch memory)
         const uint32_t wd[8] = {chc0.x, chc0.y, chc0.z, chc0.w, chc1.x, chc1.y, chc1.z, chc1.w};
-        const uint32_t xt = tid * (uint32_t)kEBytes;
-        // the literal starts among the thread's bytes (bit j: byte xt + j starts a literal; empty
-        // literals add nothing) and the bytes it owns: masks, so the byte loops below have no
-        // control flow and their table reads issue back to back
+        // the literal starts among the thread's bytes after its first (bit j: byte xt + j starts a
+        // literal; empty literals add nothing) and the bytes it owns: masks, so the byte loops below have
+        // no control flow and their table reads issue back to back
         uint32_t bm = 0, vm = 0, em = 0;  // em bit j: byte xt + j is the last of its literal
-        // every literal the thread touches has room for 30 bits per byte (the longest code): pass 2
-        // needs no capacity check
-        auto lit_safe = [&](uint32_t l) {
-            return (S.ooff[l + 1] - S.ooff[l]) * 8u >= 30u * (S.ioff[l + 1] - S.ioff[l]);
-        };
-        bool allsafe = true;
+        bool f0 = false;       // the thread's first byte starts a literal
         bool ends_here = false;  // the thread's last literal ends at its last byte
         if (any) {
             vm = (uint32_t)(((1ull << (x1 - x0)) - 1ull) << (x0 - xt));
-            allsafe = lit_safe(li);
-            uint32_t lj = li + 1;
-            uint32_t nj = S.ioff[lj];
-            while (nj < x1) {
-                bm |= 1u << (nj - xt);
-                allsafe &= lit_safe(lj);
-                nj = S.ioff[++lj];
-            }
-            ends_here = nj == x1;
+            f0 = (sm >> (x0 - xt)) & 1u;
+            bm = sm & vm & ~(1u << (x0 - xt));
+            ends_here = x1 == xe || (snext & 1u);
             em = (bm >> 1) | (ends_here ? 1u << (x1 - 1u - xt) : 0u);
         }
         // pass 2's run starts: the literal starts, the tile's first byte when the thread holds bytes
@@ -328,39 +370,47 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
             }
         }
         EPROF(3);
-        // segmented exclusive scan over the workgroup: the carry into each thread's first literal
-        uint32_t fi = f, vi = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t pf = __shfl_up(fi, d), pv = __shfl_up(vi, d);
-            if (lane >= (uint32_t)d) {
-                vi = fi ? vi : vi + pv;
-                fi |= pf;
-            }
-        }
+        // segmented exclusive scan over the workgroup: the carry into each thread's first literal, and
+        // (max scan) 1 + the last literal starting before the thread's bytes
+        uint32_t fi = f, vi = v, Li = sl;
+        wave_seg_scan(fi, vi, Li, lane);
         if (lane == 63) {
             S.wf[wv] = fi;
             S.wv[wv] = vi;
+            S.wl[wv] = Li;
         }
+        EPROF(4);
         lds_barrier_e();
-        uint32_t cw = 0;  // carry into this wave's lane 0 (the waves' totals read together)
+        EPROF(11);
+        uint32_t cw = 0, cl = 0;  // carry into this wave's lane 0 (the waves' totals read together)
 #pragma unroll
         for (uint32_t j = 0; j < (uint32_t)kEB / 64u - 1u; ++j) {
-            const uint32_t f = S.wf[j], v = S.wv[j];
-            if (j < wv) cw = f ? v : cw + v;
+            const uint32_t f = S.wf[j], v = S.wv[j], l = S.wl[j];
+            if (j < wv) {
+                cw = f ? v : cw + v;
+                cl = max(cl, l);
+            }
         }
-        uint32_t ef = __shfl_up(fi, 1), ev = __shfl_up(vi, 1);
-        if (lane == 0) {
-            ef = 0;
-            ev = 0;
-        }
+        const uint32_t ef = dpp_e<0x138>(fi), ev = dpp_e<0x138>(vi), el = dpp_e<0x138>(Li);  // wave_shr:1 (lane 0: 0)
         const uint32_t carry = ef ? ev : cw + ev;
+        const uint32_t lx = max(cl, el);  // 1 + the last non-empty literal starting before byte xt
+        // the literal holding x0: the one starting there (after any empty ones), else the last one
+        // started before it
+        uint32_t li = 0;
+        if (any) {
+            if (f0) {
+                li = lx;
+                while (S.ioff[li + 1] <= x0) ++li;
+            } else {
+                li = lx - 1u;
+            }
+        }
         // pass 2: each run of codes (this thread's bytes of one literal) is packed into a 64-bit
         // accumulator aligned to the image's dword grid: whole dwords inside the run are plain
         // stores, the run's first and last (shared with neighbouring runs) are ds_or; a code past
         // the literal's capacity is clipped (rare: the caller's capacity below the bound)
         EPROF(4);
-        if (__all(allsafe)) {
+        if (tile_safe) {
             // v3 pass 2 (every literal of the wave's threads has room): per byte, the code is shifted
             // into a 64-bit accumulator holding the bits of the current image dword on (n of them,
             // counted from the dword's start: a run that starts mid-dword begins with n zero bits
@@ -496,8 +546,9 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
             }
             flush_run();
         }
-        lds_barrier_e();
         EPROF(5);
+        lds_barrier_e();
+        EPROF(11);
         // per literal: EOS padding, out_len, status
 #pragma unroll
         for (int r = 0; r < kEMeta; ++r) {
@@ -523,8 +574,9 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
                 }
             }
         }
-        lds_barrier_e();
         EPROF(6);
+        lds_barrier_e();
+        EPROF(11);
         {  // write the image back: bytes [G0, G1) of the image (relative to ob16)
             const uint32_t G0 = S.ooff[0], G1 = S.ooff[k];
             const uint32_t c1 = (G1 + 15u) >> 4;
@@ -560,7 +612,7 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
     }
     if (kProf) {
         __syncthreads();
-        if (tid < (kEB / 64) * 9) atomicAdd(&a.prof[tid % 9], S.prof[tid / 9][tid % 9]);
+        if (tid < (kEB / 64) * 12) atomicAdd(&a.prof[tid % 12], S.prof[tid / 12][tid % 12]);
     }
 }
 
@@ -603,7 +655,7 @@ int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
     }
 #endif
     // per = workgroups per CU; fewer when the batch is small (>= ~64 literals per workgroup)
-    const int per = (cfg == 1 || cfg == 2) ? 1 : 2;
+    const int per = cfg == 1 ? 1 : 2;
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
     if (blocks > (uint64_t)c->num_cu * per) blocks = (uint64_t)c->num_cu * per;
     if (blocks < 1) blocks = 1;
@@ -612,12 +664,6 @@ int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
 #ifdef HPK_DIAG
         case 1:  // one 1024-thread workgroup per CU, 32 KiB tiles
             hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 32>), grid, dim3(1024), 0, c->stream, a);
-            break;
-        case 2:  // one 1024-thread workgroup per CU, 16 bytes per thread
-            hipLaunchKernelGGL((hpk_encode2<1024, 112 * 1024, 2048, 16>), grid, dim3(1024), 0, c->stream, a);
-            break;
-        case 3:  // two 512-thread workgroups per CU, 16 bytes per thread
-            hipLaunchKernelGGL((hpk_encode2<512, 56 * 1024, 1024, 16>), grid, dim3(512), 0, c->stream, a);
             break;
         case 9:  // the product geometry with per-phase cycle counters (hpk_debug_encode_prof)
             if (!g_eprof) HIP_TRY(hipMalloc(&g_eprof, 16 * sizeof(unsigned long long)));

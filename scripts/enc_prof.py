@@ -18,7 +18,8 @@ import torch  # noqa: E402
 from loona_amd import HuffmanCodec, _lib, synth  # noqa: E402
 from loona_amd.batch import encode_offsets_torch  # noqa: E402
 
-PHASES = ["top_barriers", "meta_fits", "search_setup", "pass1", "scan", "pass2", "finalize", "writeback", "split"]
+PHASES = ["top", "meta_fits", "setup", "pass1", "scan", "pass2", "finalize", "writeback", "split", "unused9",
+          "unused10", "barrier_waits"]  # (v5: the barriers' waits apart from the phases' work)
 
 
 def main():
@@ -38,7 +39,7 @@ def main():
     L.hpk_debug_encode_prof.argtypes = [ctypes.c_void_p]
     buf = np.zeros(16, np.uint64)
     assert L.hpk_debug_encode_prof(buf.ctypes.data) == 0
-    tot = float(buf[:9].sum())
+    tot = float(buf[:12].sum())
     print(json.dumps({"workload": wl, "cycles_total": tot,
                       "share": {p: round(float(buf[i]) / tot, 4) for i, p in enumerate(PHASES)}}), flush=True)
 

@@ -470,6 +470,41 @@ def test_encode_small_capacity_and_huge_literal(codec):
     assert (o[int(oo[-1]) :] == 0xAB).all()
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_encode_mixed_regions_and_empty_runs(codec, seed):
+    """Encode v5 finds a thread's literal starts in a per-tile start map and the literal holding its
+    first byte by a max scan, and picks the checked pass 2 per tile: tiles mixing bound-sized and exact
+    regions, runs of empty literals (several literals starting at one byte), 1-byte literals (up to 32
+    starts in one thread's bytes) and literals crossing many threads."""
+    from hpk_util import oracle_encode
+
+    rng = np.random.default_rng(100 + seed)
+    lens = rng.choice([0, 1, 2, 5, 31, 32, 33, 200, 1500], size=6000, p=[.2, .2, .1, .1, .1, .1, .1, .08, .02])
+    lens[100:140] = 0
+    lens[500:900] = 1
+    strs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in lens]
+    want = [oracle_encode(x) for x in strs]
+    blob, off = pack(strs)
+    n = len(strs)
+    # exact regions for every third literal after 2,000, bound regions (30 bits per byte) otherwise
+    cap = np.array([len(w) if (i >= 2000 and i % 3 == 0) else (30 * len(s) + 7) // 8 for i, (s, w) in
+                    enumerate(zip(strs, want))], np.int64)
+    oo = np.zeros(n + 1, np.int64)
+    np.cumsum(cap, out=oo[1:])
+    dblob, doff = to_dev(blob), to_dev(off.astype(np.int32))
+    doo = to_dev(oo.astype(np.int32))
+    out = torch.full((int(oo[-1]) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+    codec.encode_into(dblob, doff, out, doo, ol, st, device=True, sync=True)
+    o, oln, stn = out.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy()
+    assert not stn.any()
+    for i in range(n):
+        assert int(oln[i]) == len(want[i]), i
+        assert o[oo[i] : oo[i] + oln[i]].tobytes() == want[i], i
+    assert (o[int(oo[-1]) :] == 0xAB).all()
+
+
 def test_config2_full_roundtrip(codec):
     """BASELINE config 2 at full size (1M literals): GPU decode of the canonical encoding gives back
     the generated strings exactly (size-independent property); a 100k prefix is also compared to
