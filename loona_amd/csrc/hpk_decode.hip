@@ -347,8 +347,16 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
         return hpk_long_list_used(c, lslot);
     }
     if (wave) {
+        // (every mode runs the kernel the product would: fixed chunks below HPK_WAVE_GUIDED_MIN literals)
+#define WAVE_LAUNCH(m)                                                                    \
+    do {                                                                                  \
+        if (b.n < HPK_WAVE_GUIDED_MIN)                                                    \
+            hipLaunchKernelGGL(WAVE_KERNEL_SMALL(m), grid, block, 0, c->stream, a);       \
+        else                                                                              \
+            hipLaunchKernelGGL(WAVE_KERNEL(m), grid, block, 0, c->stream, a);             \
+    } while (0)
         if (g_debug_mode == 1) {
-            hipLaunchKernelGGL(WAVE_KERNEL(1), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(1);
         } else if (g_debug_mode == 3) {
             const size_t need = (size_t)blocks * kWaves * 16;
             if (need > g_dbg_n) {
@@ -357,21 +365,36 @@ int hpk_launch_decode(hpk_ctx* c, const hpk_batch& b) {
                 g_dbg_n = need;
             }
             a.dbg = g_dbg;
-            hipLaunchKernelGGL(WAVE_KERNEL(3), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(3);
         } else if (g_debug_mode == 2)
-            hipLaunchKernelGGL(WAVE_KERNEL(2), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(2);
         else if (g_debug_mode == 6)
-            hipLaunchKernelGGL(WAVE_KERNEL(6), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(6);
         else if (g_debug_mode == 7)
-            hipLaunchKernelGGL(WAVE_KERNEL(7), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(7);
         else if (g_debug_mode == 8)  // LDS conflict attribution (lit12_body's kDup): table reads twice
-            hipLaunchKernelGGL(WAVE_KERNEL(8), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(8);
         else if (g_debug_mode == 9)  // the window read twice
-            hipLaunchKernelGGL(WAVE_KERNEL(9), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(9);
         else if (g_debug_mode == 10)  // the byte stores twice
-            hipLaunchKernelGGL(WAVE_KERNEL(10), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(10);
+        else if (g_debug_mode == 5) {  // per-wave counters of the long-literal phase (HPK_LONG_WAVES waves)
+            const size_t need = (size_t)blocks * HPK_LONG_WAVES * 16;
+            if (need > g_dbg_n) {
+                (void)hipFree(g_dbg);
+                HIP_TRY(hipMalloc(&g_dbg, need * 8));
+                g_dbg_n = need;
+            }
+            HIP_TRY(hipMemsetAsync(g_dbg, 0, need * 8, c->stream));
+            a.dbg = g_dbg;
+            if (b.n < HPK_WAVE_GUIDED_MIN)
+                hipLaunchKernelGGL(WAVE_KERNEL_SMALL(5), grid, block, 0, c->stream, a);
+            else
+                WAVE_LAUNCH(5);
+        } else if (b.n < HPK_WAVE_GUIDED_MIN)  // (the product's choice)
+            hipLaunchKernelGGL(WAVE_KERNEL_SMALL(0), grid, block, 0, c->stream, a);
         else
-            hipLaunchKernelGGL(WAVE_KERNEL(0), grid, block, 0, c->stream, a);
+            WAVE_LAUNCH(0);
         HIP_TRY(hipGetLastError());
         return hpk_long_list_used(c, lslot);
     }

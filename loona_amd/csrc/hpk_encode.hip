@@ -209,7 +209,17 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
         uint4* i16 = reinterpret_cast<uint4*>(S.img);
         for (uint32_t c = tid; c < (uint32_t)kEO / 16; c += kEB) i16[c] = make_uint4(0, 0, 0, 0);
     }
-    // the workgroup's literals: equal input bytes (+ 16 per literal) per workgroup
+    if (tid == 0) {
+        S.ctr[0] = 0;
+        S.ctr[1] = 0;
+        S.ctr[2] = 0;
+    }
+    for (uint32_t w = tid; w <= (uint32_t)kEB; w += kEB) {
+        S.smap[w] = 0;
+        S.slast[w] = 0;
+    }
+    // the workgroup's literals: equal input bytes (+ 16 per literal) per workgroup (split_by_bytes has
+    // barriers: the clears above are seen by the first tile)
     uint32_t BA, BB;
     hpksplit::split_by_bytes<kEB, 16>(a.in_off, a.n, S.split, BA, BB);
     EPROF(8);
@@ -246,19 +256,10 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
         EPROF(7);
         lds_barrier_e();  // the previous tile's image is out
         EPROF(11);
-        if (tid == 0) {
-            S.ctr[0] = 0;
-            S.ctr[1] = 0;
-            S.ctr[2] = 0;
-        }
+        // (the counters and the start map were cleared after the previous tile's scan, or before the first
+        // tile; the live map is first written in finalize, barriers later: v5b, one barrier fewer per tile)
         for (uint32_t w = tid; w < (uint32_t)((kEO / 16 + 31) / 32); w += kEB) S.live[w] = 0;
-        for (uint32_t w = tid; w <= (uint32_t)kEB; w += kEB) {
-            S.smap[w] = 0;
-            S.slast[w] = 0;
-        }
         EPROF(0);
-        lds_barrier_e();
-        EPROF(11);
         // which literals fit (a prefix: offsets are non-decreasing); each fitting non-empty literal marks
         // its first byte in the start map and its index in its word's slast
         uint32_t kw = 0;
@@ -393,6 +394,17 @@ __global__ __launch_bounds__(kEB, 4) void hpk_encode2(EncodeArgs a) {
         }
         const uint32_t ef = dpp_e<0x138>(fi), ev = dpp_e<0x138>(vi), el = dpp_e<0x138>(Li);  // wave_shr:1 (lane 0: 0)
         const uint32_t carry = ef ? ev : cw + ev;
+        // every thread has read the counters and its start-map words (before the barrier above): clear them
+        // for the next tile
+        if (tid == 0) {
+            S.ctr[0] = 0;
+            S.ctr[1] = 0;
+            S.ctr[2] = 0;
+        }
+        for (uint32_t w = tid; w <= (uint32_t)kEB; w += kEB) {
+            S.smap[w] = 0;
+            S.slast[w] = 0;
+        }
         const uint32_t lx = max(cl, el);  // 1 + the last non-empty literal starting before byte xt
         // the literal holding x0: the one starting there (after any empty ones), else the last one
         // started before it

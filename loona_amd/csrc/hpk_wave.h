@@ -329,7 +329,9 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
             if (lane == 0) {
                 const uint32_t seen = *(volatile HPK_LDS_AS uint32_t*)(&s_ctr[7]);
                 const uint32_t left = BB - BA > seen ? BB - BA - seen : 0u;
-                const uint32_t want = kGuided == 2 ? kChunk : max(kChunk, left / 32u);  // (2: fixed chunks)
+                // (2: fixed chunks. Round 6: fixed chunks until 16 were left, then 1/16 of what was left, at
+                // least 32 / 48 / 64 literals: config 2 47.1-47.8 / 45.2-45.5 / 44.1-44.6 vs 40.5-41.4 us)
+                const uint32_t want = kGuided == 2 ? kChunk : max(kChunk, left / 32u);
                 c = atomicAdd(&s_ctr[7], want);
                 c = c < BB - BA ? c : BB - BA;
                 ce = BA + min(c + want, BB - BA);  // (lane 0's; broadcast below)
@@ -914,7 +916,7 @@ __global__ __launch_bounds__(1024) void hpk_decode_wave(DecodeArgs a) {
         constexpr int kLB = HPK_LONG_WAVES * 64;  // the fill kernel's geometry (hpk_long.h)
         constexpr int kLQ = kLB * (HPK_LONG_RING * 4 + HPK_LONG_OS);
         static_assert(kLQ + HPK_LONG_WAVES * HPK_LONG_CLAIM * 16 <= G::kWaves * G::kWaveBytes, "long-phase LDS");
-        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, kTab>(
+        long_phase<kLB, HPK_LONG_U, HPK_LONG_RING, kMode == 5 ? 1 : 0, G::kBlock, HPK_LONG_OS, HPK_LONG_CLAIM, kTab>(
             a, BA, BB, c1, c2, &s_ctr[3], reinterpret_cast<uint32_t*>(area), area + kLB * HPK_LONG_RING * 4,
             reinterpret_cast<uint4*>(area + kLQ), s_lut, s_lo);
     }

@@ -69,4 +69,15 @@ if mode == 5:  # hpk_decode_long's per-wave counters
              "idle_first_chunks", "idle_ended", "ringwrite_wait_cyc"]
     res["long_per_wave"] = {nm: {"mean": round(float(st8[:, i].mean()), 1), "max": int(st8[:, i].max()),
                                  "min": int(st8[:, i].min())} for i, nm in enumerate(names)}
+    # (round 6) per workgroup (8 long-phase waves each): its slowest wave and its total lane-steps, to tell
+    # imbalance across workgroups from imbalance inside one
+    if st8.shape[0] % 8 == 0:
+        g = st8.reshape(-1, 8, 16)
+        wmax, wmean, work = g[:, :, 0].max(1), g[:, :, 0].mean(1), g[:, :, 2].sum(1)
+        res["per_workgroup"] = {
+            "slowest_wave_cycles": {"mean": round(float(wmax.mean()), 1), "max": int(wmax.max()), "min": int(wmax.min())},
+            "mean_wave_cycles": {"mean": round(float(wmean.mean()), 1), "max": round(float(wmean.max()), 1)},
+            "lane_steps": {"mean": round(float(work.mean()), 1), "max": int(work.max()), "min": int(work.min())},
+            "corr_lane_steps_slowest": round(float(np.corrcoef(work, wmax)[0, 1]), 3),
+            "top8_slowest": [int(x) for x in np.sort(wmax)[-8:]]}
 print(json.dumps(res), flush=True)
