@@ -126,8 +126,8 @@ int hpk_decode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
  * the kernel hands to its long- or huge-literal phase keeps a region of its 4-rounded decoded bound,
  * the bytes past its out_len unwritten: every literal of >= 64 encoded bytes, and every literal
  * (short ones too) of a workgroup range the kernel lists whole because most of its input bytes are
- * in such literals. Batches the wave-fill kernel decodes (>= 4M literals, or that kernel forced by
- * hpk_ctx_set_decode_kernel) are packed per workgroup: workgroup w's runs and listed regions fill
+ * in such literals. Batches the wave-fill kernel decodes (every batch unless the workgroup-fill kernel is
+ * forced by hpk_ctx_set_decode_kernel) are packed per workgroup: workgroup w's runs and listed regions fill
  * its literal range [a, b)'s share [U(a), U(b)) from its start, the rest of the share unwritten, where
  * U(i) = floor(8 (in_off[i] - in_off[0]) / 5) + 4 i (it holds every 4-rounded decoded bound of the
  * range), and out_off[n] = U(n); the workgroup-fill kernel packs every run from one device cursor and
@@ -150,12 +150,24 @@ int hpk_encode_batch(hpk_ctx* ctx, const uint8_t* in_blob, size_t in_cap, const 
                      uint8_t* status, int flags);
 
 /* Which decode kernel a context's batches use. All give identical results (the parity tests run
- * every case through each); they differ in speed by batch size. HPK_DECODE_AUTO (the default): the
- * workgroup-fill kernel below 4M literals, the wave-fill kernel from 4M on. */
+ * every case through each); they differ in speed. HPK_DECODE_AUTO (the default): the wave-fill kernel
+ * for every batch (since round 6; it had been the workgroup-fill kernel below 4M literals). */
 #define HPK_DECODE_AUTO 0
 #define HPK_DECODE_FILL 1 /* workgroup fills: one fill at a time per CU, barriers between fills */
 #define HPK_DECODE_WAVE 2 /* wave fills: every wave its own fills, no barriers between them */
 int hpk_ctx_set_decode_kernel(hpk_ctx* ctx, int kind);
+
+/* Small-call mode (opt-in; hpk_persist.h). A persistent kernel of `workgroups` (1-16) workgroups, its
+ * decode tables resident in LDS, takes this context's synchronous device-pointer hpk_decode_batch
+ * calls of 1..max_literals literals through a host-mapped doorbell (after the work already queued on
+ * the context's stream): such a call skips the kernel launch and the stream synchronisation.
+ * Results are identical to the launch path's (a batch with bad offsets is handed to the launch path).
+ * While the kernel runs it holds `workgroups` CUs, which the context's batch kernels then leave out.
+ * It exits after idle_ms (1-10000) without a call (the next small call starts it again), when the
+ * mode is turned off (max_literals = 0) or when the context is destroyed. No counterpart in the
+ * reference: loona decodes one connection's header block at a time (crates/loona/src/h2/server.rs:
+ * 1619-1637), the granularity this mode serves. */
+int hpk_ctx_set_small_mode(hpk_ctx* ctx, uint32_t max_literals, int workgroups, uint32_t idle_ms);
 
 /* Read and clear the context's sticky device error flag (after HPK_ASYNC calls; synchronises the
  * ctx stream). Returns HPK_E_OK, HPK_E_INVAL (some call saw bad offsets) or HPK_E_DEVICE.
@@ -347,6 +359,13 @@ void hpk_test_fail_batches(int n);
  * (n + 1 entries) into device memory out (n + 1 entries): the exclusive sum mod 2^32 of
  * (floor(8 len / 5) + 3) & ~3, synchronously on the context's stream. */
 int hpk_test_bound_scan(hpk_ctx* ctx, const uint32_t* in_off, uint32_t n, uint32_t* out);
+/* Testing only: how many decode calls of this context the small-call mode's persistent kernel has
+ * answered (hpk_ctx_set_small_mode), so the tests can tell it ran. */
+uint64_t hpk_test_small_calls(const hpk_ctx* ctx);
+/* Testing only: the small-call mode's device stamps of its last request (100 MHz ticks): workgroup 0 saw
+ * it, broadcast it, finished its literals; the last workgroup published it; then workgroup 0's shader-clock
+ * cycles from the broadcast to its finish and the same interval in 100 MHz ticks (6 values). */
+int hpk_test_small_stamps(const hpk_ctx* ctx, uint32_t* out6);
 
 /* Library/kernel identification (for logs and the bench JSON). */
 const char* hpk_version(void);

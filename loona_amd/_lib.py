@@ -81,7 +81,10 @@ EXPORTS = (
     "hpk_henc_out_free",
     "hpk_test_fail_batches",
     "hpk_test_bound_scan",
+    "hpk_test_small_calls",
+    "hpk_test_small_stamps",
     "hpk_ctx_set_decode_kernel",
+    "hpk_ctx_set_small_mode",
     "hpk_version",
 )
 
@@ -229,10 +232,18 @@ def lib() -> ctypes.CDLL:
         L.hpk_henc_out_free.restype = None
         L.hpk_ctx_set_decode_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.hpk_ctx_set_decode_kernel.restype = ctypes.c_int
+        L.hpk_ctx_set_small_mode.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32]
+        L.hpk_ctx_set_small_mode.restype = ctypes.c_int
         # test-only entry points: bound when the library has them (an A/B build of another source may not)
         if hasattr(L, "hpk_test_fail_batches"):
             L.hpk_test_fail_batches.argtypes = [ctypes.c_int]
             L.hpk_test_fail_batches.restype = None
+        if hasattr(L, "hpk_test_small_stamps"):
+            L.hpk_test_small_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            L.hpk_test_small_stamps.restype = ctypes.c_int
+        if hasattr(L, "hpk_test_small_calls"):
+            L.hpk_test_small_calls.argtypes = [ctypes.c_void_p]
+            L.hpk_test_small_calls.restype = ctypes.c_uint64
         if hasattr(L, "hpk_test_bound_scan"):
             L.hpk_test_bound_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
             L.hpk_test_bound_scan.restype = ctypes.c_int

@@ -177,12 +177,18 @@ class HuffmanCodec:
     DECODE_KERNELS = {"auto": 0, "fill": 1, "wave": 2}
 
     def set_decode_kernel(self, kind: str):
-        """'auto' (default: workgroup fills below 4M literals, wave fills from 4M on), 'fill' or
-        'wave' (hpk_ctx_set_decode_kernel): the same
-        results, different speed by batch size."""
+        """'auto' (default: wave fills for every batch since round 6), 'fill' or 'wave'
+        (hpk_ctx_set_decode_kernel): the same results, different speed."""
         if kind not in self.DECODE_KERNELS:
             raise ValueError(f"decode kernel {kind!r} not in {tuple(self.DECODE_KERNELS)}")
         _lib.check(self._L.hpk_ctx_set_decode_kernel(self._h, self.DECODE_KERNELS[kind]), "hpk_ctx_set_decode_kernel")
+
+    def set_small_mode(self, max_literals: int, workgroups: int = 4, idle_ms: int = 50):
+        """The small-call mode (hpk_ctx_set_small_mode): synchronous device-pointer decode calls of at
+        most max_literals literals go to a persistent kernel of `workgroups` workgroups instead of a
+        launch; it exits after idle_ms without a call. max_literals = 0 turns it off."""
+        _lib.check(self._L.hpk_ctx_set_small_mode(self._h, int(max_literals), int(workgroups), int(idle_ms)),
+                   "hpk_ctx_set_small_mode")
 
     def sync(self):
         _lib.check(self._L.hpk_ctx_sync(self._h), "hpk_ctx_sync")

@@ -148,6 +148,10 @@ int hpk_long_list_used(hpk_ctx* c, int slot) {
 extern "C" void hpk_ctx_destroy(hpk_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    (void)hpk_persist_stop(c);
+    if (c->sm_stream) (void)hipStreamDestroy(c->sm_stream);
+    if (c->h_sm) (void)hipHostFree(c->h_sm);
+    (void)hipFree(c->d_sm_dev);
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->d_lut);
     (void)hipFree(c->d_lut2);
@@ -227,6 +231,32 @@ extern "C" int hpk_ctx_set_decode_kernel(hpk_ctx* c, int kind) {
 }
 
 extern "C" void* hpk_ctx_stream(hpk_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int hpk_ctx_set_small_mode(hpk_ctx* c, uint32_t max_literals, int workgroups, uint32_t idle_ms) {
+    if (!c) return HPK_E_INVAL;
+    HIP_TRY(hipSetDevice(c->device));
+    if (max_literals == 0) {
+        const int rc = hpk_persist_stop(c);
+        c->sm_max = 0;
+        return rc;
+    }
+    if (workgroups < 1 || workgroups > 16 || workgroups >= c->num_cu || idle_ms < 1 || idle_ms > 10000 ||
+        max_literals > (uint32_t)workgroups * 256u * 64u)
+        return hpk_set_err_msg("small mode: 1-16 workgroups, 1-10000 ms idle, at most 64 literals per lane", HPK_E_INVAL);
+    if (!c->h_sm) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->sm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipHostMalloc(&c->h_sm, 256, hipHostMallocMapped | hipHostMallocCoherent));
+        memset(c->h_sm, 0, 256);
+        HIP_TRY(hipHostGetDevicePointer(&c->d_sm, c->h_sm, 0));
+        HIP_TRY(hipMalloc(&c->d_sm_dev, 128));  // [0..4) counters, [4, 21) the request copy
+    }
+    if (c->sm_launched && (workgroups != c->sm_wgs || idle_ms != c->sm_idle_ms))
+        if (int rc = hpk_persist_stop(c)) return rc;
+    c->sm_max = max_literals;
+    c->sm_wgs = workgroups;
+    c->sm_idle_ms = idle_ms;
+    return c->sm_launched ? HPK_E_OK : hpk_persist_start(c);
+}
 
 extern "C" int hpk_ctx_sync(hpk_ctx* c) {
     if (!c) return HPK_E_INVAL;
@@ -381,6 +411,11 @@ static int run_batch(launch_fn fn, hpk_ctx* c, const uint8_t* in_blob, size_t in
         if (n == 0) return HPK_E_OK;
         if (!in_blob || !out_blob) return hpk_set_err_msg("null blob", HPK_E_INVAL);
         const hpk_batch b{in_blob, clamp_cap(in_cap), in_off, n, out_blob, clamp_cap(out_cap), out_off, out_len, status};
+        if (fn == hpk_launch_decode && !(flags & HPK_ASYNC) && c->sm_max) {  // the small-call mode
+            bool handled = false;
+            if (int rc = hpk_persist_call(c, b, &handled)) return rc;
+            if (handled) return HPK_E_OK;
+        }
         int rc = fn(c, b);
         if (rc) return rc;
         if (!(flags & HPK_ASYNC)) {

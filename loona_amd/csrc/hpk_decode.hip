@@ -24,8 +24,11 @@
 // code with a capacity check per byte (HPK_OUTPUT_OVERFLOW).
 #include <stdlib.h>
 
+#include <chrono>
+
 
 #include "hpk_wave.h"
+#include "hpk_persist.h"
 
 using namespace hpkdec;
 
@@ -272,9 +275,88 @@ static uint32_t decode_blocks(hpk_ctx* c, const hpk_batch& b) {
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
     if (blocks < ((uint64_t)b.in_cap + 32767) / 32768) blocks = ((uint64_t)b.in_cap + 32767) / 32768;
     if (blocks > (uint64_t)b.n) blocks = (uint64_t)b.n;
-    if (blocks > (uint64_t)c->num_cu) blocks = (uint64_t)c->num_cu;
+    // (the small-call mode's persistent workgroups hold sm_wgs CUs: a one-per-CU grid leaves them out, or its
+    // last workgroups would wait for a CU the whole time)
+    const uint64_t cus = (uint64_t)c->num_cu - (c->sm_launched && c->sm_max ? (uint64_t)c->sm_wgs : 0u);
+    if (blocks > cus) blocks = cus;
     if (blocks < 1) blocks = 1;
     return (uint32_t)blocks;
+}
+
+// ---- the small-call mode (hpk_persist.h) ----
+constexpr int kPersistThreads = 256;
+
+static int persist_launch(hpk_ctx* c, uint32_t base) {
+    auto* h = static_cast<PersistCtl*>(c->h_sm);
+    if (c->sm_launched) HIP_TRY(hipStreamSynchronize(c->sm_stream));  // (the previous kernel has exited)
+    __atomic_store_n(&h->stop, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&h->done, base, __ATOMIC_RELAXED);
+    __atomic_store_n(&h->declined, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&h->alive, 1u, __ATOMIC_RELEASE);
+    const uint32_t init[4] = {0u, base, 0u, 0u};
+    HIP_TRY(hipMemcpyAsync(c->d_sm_dev, init, sizeof init, hipMemcpyHostToDevice, c->sm_stream));
+    PersistArgs a{static_cast<PersistCtl*>(c->d_sm), c->d_sm_dev, c->d_lut3, c->d_lo, base, c->sm_idle_ms * 100000u};
+    hipLaunchKernelGGL(hpk_persist<kPersistThreads>, dim3((uint32_t)c->sm_wgs), dim3(kPersistThreads), 0, c->sm_stream, a);
+    HIP_TRY(hipGetLastError());
+    c->sm_launched = true;
+    return HPK_E_OK;
+}
+
+int hpk_persist_start(hpk_ctx* c) { return persist_launch(c, c->sm_req); }
+
+extern "C" uint64_t hpk_test_small_calls(const hpk_ctx* c) { return c ? c->sm_calls : 0u; }
+
+extern "C" int hpk_test_small_stamps(const hpk_ctx* c, uint32_t* out6) {
+    if (!c || !c->h_sm || !out6) return HPK_E_INVAL;
+    const auto* h = static_cast<const PersistCtl*>(c->h_sm);
+    for (int k = 0; k < 6; ++k) out6[k] = __atomic_load_n(&h->ts[k], __ATOMIC_ACQUIRE);
+    return HPK_E_OK;
+}
+
+int hpk_persist_stop(hpk_ctx* c) {
+    if (!c->sm_launched) return HPK_E_OK;
+    auto* h = static_cast<PersistCtl*>(c->h_sm);
+    __atomic_store_n(&h->stop, 1u, __ATOMIC_RELEASE);
+    HIP_TRY(hipStreamSynchronize(c->sm_stream));
+    c->sm_launched = false;
+    return HPK_E_OK;
+}
+
+int hpk_persist_call(hpk_ctx* c, const hpk_batch& b, bool* handled) {
+    *handled = false;
+    if (!c->sm_max || b.n > c->sm_max || b.n == 0) return HPK_E_OK;
+    // the kernel does not follow the caller's stream order: the work queued there before this call (a
+    // synchronous call waits for it anyway) is finished first
+    if (hipStreamQuery(c->stream) != hipSuccess) HIP_TRY(hipStreamSynchronize(c->stream));
+    auto* h = static_cast<PersistCtl*>(c->h_sm);
+    if (!c->sm_launched || __atomic_load_n(&h->alive, __ATOMIC_ACQUIRE) == 0u)
+        if (int rc = persist_launch(c, c->sm_req)) return rc;
+    const uintptr_t ip = (uintptr_t)b.in_blob, op = (uintptr_t)b.out_blob;
+    h->in_base = (const uint8_t*)(ip & ~(uintptr_t)15);
+    h->out_base = (uint8_t*)(op & ~(uintptr_t)15);
+    h->in_off = b.in_off;
+    h->out_off = b.out_off;
+    h->out_len = b.out_len;
+    h->status = b.status;
+    h->n = b.n;
+    h->in_mis = (uint32_t)(ip & 15);
+    h->out_mis = (uint32_t)(op & 15);
+    h->in_cap = b.in_cap;
+    h->out_cap = b.out_cap;
+    const uint32_t k = ++c->sm_req;
+    __atomic_store_n(&h->req, k, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 0; __atomic_load_n(&h->done, __ATOMIC_ACQUIRE) != k; ++spins) {
+        if (__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE) == 0u) {  // it went idle just before the request
+            if (int rc = persist_launch(c, k - 1u)) return rc;
+        }
+        __builtin_ia32_pause();
+        if ((spins & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+            return hpk_set_err_msg("small-call mode: the persistent kernel did not answer", HPK_E_DEVICE);
+    }
+    *handled = __atomic_load_n(&h->declined, __ATOMIC_ACQUIRE) == 0u;  // (declined: bad offsets, the launch path's)
+    c->sm_calls += *handled ? 1u : 0u;
+    return HPK_E_OK;
 }
 
 // The compacted form: the wave-fill kernel's (each workgroup packs into its range's bound span, no device

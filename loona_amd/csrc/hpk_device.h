@@ -63,7 +63,26 @@ struct hpk_ctx {
     void* cp_tmp[kLongSlots] = {};
     size_t cp_tmp_cap[kLongSlots] = {};
     uint32_t* cp_cursor[kLongSlots] = {};
+    // the small-call mode (hpk_ctx_set_small_mode, hpk_persist.h): a persistent kernel of sm_wgs
+    // workgroups on its own stream takes synchronous device-pointer batches of <= sm_max literals
+    uint32_t sm_max = 0;
+    int sm_wgs = 0;
+    uint32_t sm_idle_ms = 0;
+    hipStream_t sm_stream = nullptr;
+    void* h_sm = nullptr;           // hpkdec::PersistCtl, coherent host memory
+    void* d_sm = nullptr;           // its device-visible address
+    uint32_t* d_sm_dev = nullptr;   // [0] workgroups finished, [1] command broadcast, [2] declined request
+    uint32_t sm_req = 0;            // the last request issued
+    bool sm_launched = false;       // a kernel was launched on sm_stream (it may have exited since)
+    uint64_t sm_calls = 0;          // calls it answered (hpk_test_small_calls)
 };
+
+// The small-call mode (hpk_decode.hip): hpk_persist_call decodes a synchronous device-pointer batch through
+// the persistent kernel if the mode is on, the batch small enough and the caller's stream idle (*handled);
+// hpk_persist_stop ends the kernel and waits for it.
+int hpk_persist_call(hpk_ctx* c, const struct hpk_batch& b, bool* handled);
+int hpk_persist_start(hpk_ctx* c);
+int hpk_persist_stop(hpk_ctx* c);
 
 // The long-literal list for the context's current stream, sized for n literals (allocated on
 // first use; HPK_E_OK or an error code); *slot is passed to hpk_long_list_used after the launch.

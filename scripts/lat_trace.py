@@ -24,6 +24,10 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     codec = HuffmanCodec(0, stream="own")
     L = _lib.lib()
+    small = os.environ.get("HPK_SMALL_MODE")  # "max,workgroups,idle_ms": the small-call mode (round 6)
+    if small:
+        mx, wgs, idle = (int(x) for x in small.split(","))
+        codec.set_small_mode(mx, wgs, idle)
     w = synth.device_config2(codec, n=20000, seed=91)
     res = []
     for n in (1000, 5000, 20000):
@@ -41,13 +45,25 @@ def main():
         for _ in range(20):
             assert fn(*args) == 0
         ts = []
+        dv = []  # (small-call mode) the device stamps' intervals, us
+        st4 = (ctypes.c_uint32 * 6)()
         for _ in range(reps):
             t0 = time.perf_counter()
             fn(*args)
             ts.append(time.perf_counter() - t0)
+            if small:
+                L.hpk_test_small_stamps(codec._h, st4)
+                dv.append([((st4[k + 1] - st4[k]) & 0xFFFFFFFF) / 100.0 for k in range(3)] +
+                          [st4[4] / max(st4[5], 1) * 0.1])  # shader clock, GHz
         assert not st.any().item()
-        res.append({"lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")), "literals": n, "calls": reps, "median_us": round(statistics.median(ts) * 1e6, 1),
+        assert torch.equal(ol.to(torch.int64), (w.dec_off[1 : n + 1] - w.dec_off[:n]).to(torch.int64))
+        res.append({"lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")), "small_mode": small or None,
+                    "small_calls": int(L.hpk_test_small_calls(codec._h)) if hasattr(L, "hpk_test_small_calls") else None,
+                    "literals": n, "calls": reps, "median_us": round(statistics.median(ts) * 1e6, 1),
                     "p10_us": round(sorted(ts)[reps // 10] * 1e6, 1), "p90_us": round(sorted(ts)[reps * 9 // 10] * 1e6, 1)})
+        if dv:
+            res[-1]["device_us_median"] = {k: round(statistics.median(x[i] for x in dv), 2)
+                                           for i, k in enumerate(("broadcast", "decode_wg0", "last_publish", "sclk_ghz"))}
     for r in res:
         print(json.dumps(r), flush=True)
 

@@ -15,21 +15,28 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module", params=["fill", "wave", "compact", "compact_wave"])
+@pytest.fixture(scope="module", params=["fill", "wave", "compact", "compact_wave", "small"])
 def codec(request):
     """A device codec; every test runs with each decode kernel (hpk_ctx_set_decode_kernel: the
-    workgroup fills and the wave fills) and in the compacted-output form (hpk_decode_batch_compact,
+    workgroup fills and the wave fills), in the compacted-output form (hpk_decode_batch_compact,
     through gpu_decode / _device_decode) under each kernel (tests that pass their own output regions
-    run the region form of that kernel there), which must all give identical results."""
+    run the region form of that kernel there), and in the small-call mode (hpk_ctx_set_small_mode:
+    synchronous device calls of up to 64k literals answered by the persistent kernel), which must all
+    give identical results."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a GPU (run with -m 'not gpu' on CPU)")
-    from loona_amd import HuffmanCodec
+    from loona_amd import HuffmanCodec, _lib
 
     c = HuffmanCodec(0, stream=torch.cuda.current_stream())
-    c.set_decode_kernel({"compact": "fill", "compact_wave": "wave"}.get(request.param, request.param))
+    c.set_decode_kernel({"compact": "fill", "compact_wave": "wave", "small": "auto"}.get(request.param, request.param))
     c.compact = request.param.startswith("compact")
     c.variant = request.param
+    if request.param == "small":
+        c.set_small_mode(65536, 4, 200)
     yield c
+    if request.param == "small":
+        assert _lib.lib().hpk_test_small_calls(c._h) > 0, "the small-call mode answered no call"
+        c.set_small_mode(0)
     c.close()
 
 
@@ -1248,3 +1255,59 @@ def test_compact_unaligned_bases(codec, shift):
     for i in range(n):
         a, m = int(oon[i]), int(lw[i])
         assert bytes(outn[a : a + m]) == bytes(want[0][wo[i] : wo[i] + m]), f"literal {i}"
+
+
+def test_small_mode_idle_restart_bad_offsets_and_off(codec):
+    """The small-call mode (hpk_ctx_set_small_mode): calls answered by the persistent kernel give the
+    oracle's bytes; after its idle exit the next call starts it again; a batch with bad offsets is handed
+    to the launch path (the call fails as in the launch path, nothing is written outside the blobs);
+    turned off, calls go to the launch path. Runs once (the fixture's small variant)."""
+    if codec.variant != "small":
+        pytest.skip("small-call mode case: once")
+    import time
+
+    from loona_amd import _lib
+    from loona_amd.batch import decode_offsets_torch
+
+    L = _lib.lib()
+    rng = np.random.default_rng(41)
+    strs = [bytes(rng.choice(list(b"abcdefghijklmnopqrstuvwxyz0123456789-/.:;="), int(k))) for k in rng.integers(0, 70, 1000)]
+    from hpk_util import oracle_encode
+
+    lits = [oracle_encode(x) for x in strs]
+    lits += [bytes.fromhex(k["in"]) for k in load("kat.json")]
+    blob, off = pack(lits)
+    want = oracle_decode_batch(blob, off)
+
+    def run(expect_small):
+        before = L.hpk_test_small_calls(codec._h)
+        got = gpu_decode(codec, blob, off)
+        compare_batches(got, want, "small mode")
+        assert (L.hpk_test_small_calls(codec._h) - before == 1) == expect_small
+
+    codec.set_small_mode(4096, 2, 2)  # (2 ms idle)
+    run(True)
+    time.sleep(0.05)  # the kernel has exited
+    run(True)
+    run(True)
+    # bad offsets: the launch path's result and error
+    n = len(lits)
+    dblob = to_dev(blob)
+    bad = np.asarray(off, np.int64).copy()
+    bad[n // 2] = bad[n // 2 + 1] + 1  # a decreasing pair
+    doff = to_dev(bad.astype(np.int32))
+    oo = decode_offsets_torch(to_dev(np.asarray(off, np.int64).astype(np.int32)))
+    out = torch.full((int(oo[-1].item()) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    ol = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    before = L.hpk_test_small_calls(codec._h)
+    with pytest.raises(Exception):
+        codec.decode_into(dblob, doff, out, oo, ol, st, device=True, sync=True)
+    assert L.hpk_test_small_calls(codec._h) == before
+    assert (st.cpu().numpy() == 5).any()  # HPK_BAD_OFFSETS, from the launch path
+    assert (out[int(oo[-1].item()):].cpu().numpy() == 0xAB).all()
+    run(True)  # the mode still answers after a declined batch
+    codec.set_small_mode(0)
+    run(False)
+    codec.set_small_mode(65536, 4, 200)
+    run(True)
