@@ -364,7 +364,8 @@ int hpk_test_bound_scan(hpk_ctx* ctx, const uint32_t* in_off, uint32_t n, uint32
 uint64_t hpk_test_small_calls(const hpk_ctx* ctx);
 /* Testing only: the small-call mode's device stamps of its last request (100 MHz ticks): workgroup 0 saw
  * it, broadcast it, finished its literals; the last workgroup published it; then workgroup 0's shader-clock
- * cycles from the broadcast to its finish and the same interval in 100 MHz ticks (6 values). */
+ * cycles from the broadcast to its finish and the same interval in 100 MHz ticks; thread 0's first literal in
+ * shader-clock cycles: offsets loaded, staged, walked, stored (10 values). */
 int hpk_test_small_stamps(const hpk_ctx* ctx, uint32_t* out6);
 
 /* Library/kernel identification (for logs and the bench JSON). */

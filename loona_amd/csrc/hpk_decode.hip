@@ -306,10 +306,11 @@ int hpk_persist_start(hpk_ctx* c) { return persist_launch(c, c->sm_req); }
 
 extern "C" uint64_t hpk_test_small_calls(const hpk_ctx* c) { return c ? c->sm_calls : 0u; }
 
-extern "C" int hpk_test_small_stamps(const hpk_ctx* c, uint32_t* out6) {
+extern "C" int hpk_test_small_stamps(const hpk_ctx* c, uint32_t* out6) {  // (10 values)
     if (!c || !c->h_sm || !out6) return HPK_E_INVAL;
     const auto* h = static_cast<const PersistCtl*>(c->h_sm);
     for (int k = 0; k < 6; ++k) out6[k] = __atomic_load_n(&h->ts[k], __ATOMIC_ACQUIRE);
+    for (int k = 0; k < 4; ++k) out6[6 + k] = __atomic_load_n(&h->tl[k], __ATOMIC_ACQUIRE);
     return HPK_E_OK;
 }
 

@@ -34,7 +34,9 @@ struct PersistCtl {  // host memory (hipHostMallocMapped | hipHostMallocCoherent
     uint32_t ts[6];     // device: 100 MHz stamps of the last request (hpk_test_small_stamps): workgroup 0 saw it,
                         // broadcast it, finished its literals; the last workgroup published it; then workgroup 0's
                         // shader-clock cycles between the broadcast and its finish, and the same in 100 MHz ticks
-    uint32_t pad1[7];
+    uint32_t tl[4];     // device: thread 0's first literal of the last request, shader-clock cycles from the
+                        // command to the offsets loaded, to the literal staged, to its walk done, to its stores issued
+    uint32_t pad1[3];
     // the request (written by the host before req)
     const uint8_t* in_base;
     uint8_t* out_base;
@@ -57,6 +59,15 @@ struct PersistArgs {
 
 constexpr uint32_t kPersistExit = 0xFFFFFFFFu;
 
+// The request's pointers come from memory, not from kernel arguments, so the compiler cannot tell they are
+// global and would use flat accesses, which count in lgkmcnt too: every LDS lookup of the walk then waited
+// for the output stores in flight (~27 us for one 27-byte literal per lane). Global address space, explicitly.
+#define HPK_GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ HPK_GAS T* gas(T* p) {
+    return (HPK_GAS T*)p;
+}
+
 #ifndef HPK_PERSIST_SLEEP
 #define HPK_PERSIST_SLEEP 2  // s_sleep between polls (units of 64 cycles)
 #endif
@@ -74,7 +85,7 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
 // hpk_decode_kernel.h lit_bytes_to). Returns false (nothing written) if the literal's offsets are bad.
 template <class Ld>
 __device__ bool persist_literal(const Ld& ld16, const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo,
-                                uint8_t* out_base, uint32_t out_mis, uint32_t in_mis, uint32_t p0, uint32_t p1,
+                                HPK_GAS uint8_t* out_base, uint32_t out_mis, uint32_t in_mis, uint32_t p0, uint32_t p1,
                                 uint32_t o0, uint32_t o1, uint32_t& cnt, uint32_t& st) {
     const uint32_t nbits = (p1 - p0) * 8u, cap = o1 - o0;
     const uint32_t ob = out_mis + o0;  // (out_base-relative)
@@ -90,7 +101,7 @@ __device__ bool persist_literal(const Ld& ld16, const uint32_t* __restrict__ lut
         if ((p & 7u) == 7u) {  // a group is complete: 8 bytes at once, or its bytes from ob on
             const uint32_t g = p - 7u;
             if (g >= ob)
-                *reinterpret_cast<uint64_t*>(out_base + g) = acc;
+                *(HPK_GAS uint64_t*)(out_base + g) = acc;
             else
                 for (uint32_t x = ob; x <= p; ++x) out_base[x] = (uint8_t)(acc >> (8u * (x & 7u)));
             acc = 0;
@@ -132,94 +143,128 @@ __device__ bool persist_literal(const Ld& ld16, const uint32_t* __restrict__ lut
 // instead of one per chunk crossing: the global walker above took ~30 us for a 27-byte literal), stored
 // big-endian into the lane's slot (dword j of lane t at slot[j * kThreads + t]: no bank conflicts).
 constexpr uint32_t kPersistSlotChunks = 8;  // 128 bytes per lane: literals of <= 113 bytes (else the global walk)
+constexpr uint32_t kPersistSlotMax = 113;   // (their decoded bound, 180 bytes, fits the output slot)
+
+// Output: the walk writes the literal's bytes into the lane's LDS output slot, at the byte's position on
+// the global 4-byte grid (slot byte (ob & 3) + k), and they leave it after the walk: the head's bytes up
+// to the first 4-aligned address, then every whole dword, then the tail's bytes, the stores unrolled with
+// their own registers. (Stores inside the walk made it wait for each one to complete before the next
+// group's register could be written: ~25 us for a 27-byte literal.)
+constexpr uint32_t kPersistOutDw = 48;  // output slot dwords per lane: 113 bytes decode to <= 180, + 3 of alignment, + 4
+                                        // of a body step's garbage; the last byte is the checked steps' dummy
+
+// Input slot: the lane's chunks as contiguous big-endian dwords after one pad dword (the lane walk reads
+// dword (X >> 5) - 1), lane t's at slot + t * kPersistInStride: an odd stride, so the lanes' reads of the
+// same dword fall in different banks.
+constexpr uint32_t kPersistInStride = 4u * kPersistSlotChunks + 1u;
 
 template <int kThreads>
-__device__ void persist_literal_lds(const uint4* __restrict__ g16, uint32_t last16, uint32_t* __restrict__ slot,
-                                    const uint32_t* __restrict__ lut, const uint16_t* __restrict__ lo, uint8_t* out_base,
-                                    uint32_t out_mis, uint32_t in_mis, uint32_t p0, uint32_t p1, uint32_t o0, uint32_t o1,
-                                    uint32_t& cnt, uint32_t& st) {
-    const uint32_t b0 = p0 + in_mis, nbits = (p1 - p0) * 8u, cap = o1 - o0;
-    const uint32_t c0 = b0 >> 4, nch = ((b0 + (p1 - p0) + 15u) >> 4) - c0;  // (<= kPersistSlotChunks)
+__device__ void persist_literal_lds(const HPK_GAS u32x4* __restrict__ g16, uint32_t last16, uint32_t* __restrict__ win32,
+                                    uint8_t* __restrict__ oslot, const uint32_t* __restrict__ lut,
+                                    const uint16_t* __restrict__ lo, HPK_GAS uint8_t* out_base, uint32_t out_mis,
+                                    uint32_t in_mis, uint32_t p0, uint32_t p1, uint32_t o0, uint32_t o1, uint32_t& cnt,
+                                    uint32_t& st, uint64_t* tl = nullptr) {
+    const uint32_t nbytes = p1 - p0, b0 = p0 + in_mis, nbits = nbytes * 8u, cap = o1 - o0;
+    const uint32_t c0 = b0 >> 4, nch = ((b0 + nbytes + 15u) >> 4) - c0;  // (<= kPersistSlotChunks)
     const uint32_t ob = out_mis + o0;
+    const uint32_t oa = ob & 3u;  // the output slot's first byte sits at its global address mod 4
     cnt = 0;
     st = HPK_OK;
     if (nbits == 0u) return;
-    uint4 v[kPersistSlotChunks];
+    u32x4 v[kPersistSlotChunks];
 #pragma unroll
-    for (uint32_t j = 0; j < kPersistSlotChunks; ++j) v[j] = j < nch ? g16[min(c0 + j, last16)] : make_uint4(0, 0, 0, 0);
+    for (uint32_t j = 0; j < kPersistSlotChunks; ++j) v[j] = j < nch ? g16[min(c0 + j, last16)] : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (uint32_t j = 0; j < kPersistSlotChunks; ++j) {
-        slot[(4u * j + 0u) * kThreads] = hpk_bswap32(v[j].x);
-        slot[(4u * j + 1u) * kThreads] = hpk_bswap32(v[j].y);
-        slot[(4u * j + 2u) * kThreads] = hpk_bswap32(v[j].z);
-        slot[(4u * j + 3u) * kThreads] = hpk_bswap32(v[j].w);
+        win32[1u + 4u * j] = hpk_bswap32(v[j].x);
+        win32[2u + 4u * j] = hpk_bswap32(v[j].y);
+        win32[3u + 4u * j] = hpk_bswap32(v[j].z);
+        win32[4u + 4u * j] = hpk_bswap32(v[j].w);
     }
-    // window: win holds nb bits from bit position pos of the literal on, MSB first; q the next slot dword
-    const uint32_t sb = (b0 & 15u) * 8u;  // the literal's first bit in the slot
-    uint32_t q = sb >> 5;
-    uint64_t win = ((uint64_t)slot[q * kThreads] << 32) << (sb & 31u);
-    uint32_t nb = 32u - (sb & 31u), pos = 0;
-    q += 1u;
-    uint64_t acc = 0;
-    auto emit = [&](uint32_t sym) {
-        const uint32_t p = ob + cnt;
-        acc |= (uint64_t)sym << (8u * (p & 7u));
-        if ((p & 7u) == 7u) {
-            const uint32_t g = p - 7u;
-            if (g >= ob)
-                *reinterpret_cast<uint64_t*>(out_base + g) = acc;
-            else
-                for (uint32_t x = ob; x <= p; ++x) out_base[x] = (uint8_t)(acc >> (8u * (x & 7u)));
-            acc = 0;
-        }
-        cnt += 1u;
-    };
-    while (pos < nbits) {
-        if (nb <= 32u) {  // (q stays inside the slot: past the literal's chunks it reads zeros)
-            win |= (uint64_t)slot[min(q, 4u * kPersistSlotChunks - 1u) * kThreads] << (32u - nb);
-            nb += 32u;
-            q += 1u;
-        }
-        const uint32_t w = (uint32_t)(win >> 32);
-        const uint32_t e = lut[w >> (32 - HPK_LUT_BITS)];
-        const uint32_t l0 = HPK_L3_LEN0(e);
-        uint32_t sym, len, held = 0;
-        bool eos = false;
-        if (l0 <= (uint32_t)HPK_LUT_BITS) {
-            sym = e & 0xFFu;
-            len = l0;
-            held = HPK_L3_CODES(e) == 2u ? HPK_L3_HELD(e) : 0u;
-        } else {
+    if (tl) tl[1] = __builtin_amdgcn_s_memtime();
+    const uint32_t sb = 32u + (b0 & 15u) * 8u;  // the literal's first bit in the window
+    if (cap >= (nbytes * 8u) / 5u) {
+        // a region that holds the decoded bound: the wave kernel's lane walk (body steps while >= kBodyMin
+        // bits are left, then checked steps), bytes into the output slot, unconditional stores (kPred:
+        // the dummy byte at kPersistOutDw * 4 - 1)
+        Lit12 L;
+        L.X = sb + 31u;
+        L.Eb = L.X + nbits;
+        L.o = oa;
+        L.o0 = oa;
+        L.oend = 0;
+        L.st = HPK_OK;
+        L.more = true;
+        lit12_load(L, win32);
+        bool body = L.Eb - L.X >= kBodyMin;
+        while (body) lit12_body<kPred, 3>(L, win32, lut, lo, oslot, body);
+        while (L.more) lit12_step<kPred, false, 3, true>(L, win32, lut, lo, oslot, kPersistOutDw * 4u - 1u);
+        cnt = L.o - L.o0;
+        st = lit12_status(L);
+    } else {
+        // a region below the decoded bound: code by code, the capacity checked per byte (the fill kernels'
+        // byte path, hpk_decode_kernel.h lit_bytes_to)
+        uint32_t q = sb >> 5;
+        uint64_t win = ((uint64_t)win32[q] << 32) << (sb & 31u);
+        uint32_t nb = 32u - (sb & 31u), pos = 0;
+        q += 1u;
+        while (pos < nbits) {
+            if (nb <= 32u) {  // (q stays inside the slot: past the literal's chunks it reads zeros)
+                win |= (uint64_t)win32[min(q, 4u * kPersistSlotChunks)] << (32u - nb);
+                nb += 32u;
+                q += 1u;
+            }
+            const uint32_t w = (uint32_t)(win >> 32);
+            uint32_t sym, len;
+            bool eos;
             lo_decode(w, lo, sym, len, eos);
+            const uint32_t rem = nbits - pos;
+            if (len > rem) {  // huffman.rs:128-160
+                st = residual_status(rem, w);
+                break;
+            }
+            if (eos) {  // huffman.rs:112-116
+                st = HPK_EOS_IN_STRING;
+                break;
+            }
+            if (cnt >= cap) {
+                st = HPK_OUTPUT_OVERFLOW;
+                break;
+            }
+            oslot[oa + cnt] = (uint8_t)sym;
+            cnt += 1u;
+            win <<= len;
+            nb -= len;
+            pos += len;
         }
-        const uint32_t rem = nbits - pos;
-        if (held != 0u && held <= rem && cnt + 2u <= cap) {  // two codes of <= 12 bits, both inside
-            emit(sym);
-            emit((e >> 16) & 0xFFu);
-            win <<= held;
-            nb -= held;
-            pos += held;
-            continue;
-        }
-        if (len > rem) {  // huffman.rs:128-160
-            st = residual_status(rem, w);
-            break;
-        }
-        if (eos) {  // huffman.rs:112-116
-            st = HPK_EOS_IN_STRING;
-            break;
-        }
-        if (cnt >= cap) {
-            st = HPK_OUTPUT_OVERFLOW;
-            break;
-        }
-        emit(sym);
-        win <<= len;
-        nb -= len;
-        pos += len;
     }
-    const uint32_t pe = ob + cnt;
-    for (uint32_t x = max(ob, pe & ~7u); x < pe; ++x) out_base[x] = (uint8_t)(acc >> (8u * (x & 7u)));
+    if (tl) tl[2] = __builtin_amdgcn_s_memtime();
+    // [ob, ob + cnt): head bytes up to the 4-aligned address h, whole dwords [h, t), tail bytes [t, ob + cnt)
+    const uint32_t e = ob + cnt, h = min((ob + 3u) & ~3u, e), t = max(e & ~3u, h);
+#pragma unroll
+    for (uint32_t k = 0; k < 3u; ++k)
+        if (ob + k < h) out_base[ob + k] = oslot[oa + k];
+    // the dwords: those before the first 16-aligned address h16 and from the last one t16 on singly, the
+    // 16-byte groups between as 16-byte stores (a store instruction per group, not per dword)
+    const uint32_t* const os32 = reinterpret_cast<const uint32_t*>(oslot);
+    const uint32_t base = ob - oa;  // the slot's first byte's address (4-aligned)
+    const uint32_t h16 = min((h + 15u) & ~15u, t), t16 = max(t & ~15u, h16);
+#pragma unroll
+    for (uint32_t k = 0; k < 3u; ++k)
+        if (h + 4u * k < h16) *reinterpret_cast<HPK_GAS uint32_t*>(out_base + h + 4u * k) = os32[(h - base) / 4u + k];
+#pragma unroll
+    for (uint32_t k = 0; k < kPersistOutDw / 4u; ++k)
+        if (h16 + 16u * k < t16) {
+            const uint32_t d = (h16 - base) / 4u + 4u * k;
+            *reinterpret_cast<HPK_GAS u32x4*>(out_base + h16 + 16u * k) = u32x4{os32[d], os32[d + 1u], os32[d + 2u], os32[d + 3u]};
+        }
+#pragma unroll
+    for (uint32_t k = 0; k < 3u; ++k)
+        if (t16 + 4u * k < t) *reinterpret_cast<HPK_GAS uint32_t*>(out_base + t16 + 4u * k) = os32[(t16 - base) / 4u + k];
+#pragma unroll
+    for (uint32_t k = 0; k < 3u; ++k)
+        if (t + k < e) out_base[t + k] = oslot[t + k - (ob - oa)];
+    if (tl) tl[3] = __builtin_amdgcn_s_memtime();
 }
 
 template <int kThreads>
@@ -232,7 +277,8 @@ __global__ __launch_bounds__(kThreads) void hpk_persist(PersistArgs p) {
     __shared__ uint32_t s_lut[HPK_LUT_SIZE];
     __shared__ uint16_t s_lo[HPK_LO_SIZE];
     __shared__ uint32_t s_cmd[18];
-    __shared__ uint32_t s_slot[4 * kPersistSlotChunks * kThreads];  // per lane: its literal's input (staged)
+    __shared__ uint32_t s_slot[kPersistInStride * kThreads];  // per lane: its literal's input (staged)
+    __shared__ uint32_t s_oslot[kPersistOutDw * kThreads];          // per lane: its literal's output
     const uint32_t tid = threadIdx.x, lane = tid & 63u, G = gridDim.x, wg = blockIdx.x;
     for (uint32_t t = tid; t < (uint32_t)HPK_LUT_SIZE; t += kThreads) s_lut[t] = p.lut3[t];
     for (uint32_t t = tid; t < (uint32_t)HPK_LO_SIZE; t += kThreads) s_lo[t] = p.lo[t];
@@ -301,34 +347,45 @@ __global__ __launch_bounds__(kThreads) void hpk_persist(PersistArgs p) {
         // the input and the offsets were written by kernels that finished before the call: one acquire
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         auto ptr = [&](int k) { return ((uint64_t)s_cmd[k + 1] << 32) | s_cmd[k]; };
-        const uint8_t* in_base = reinterpret_cast<const uint8_t*>(ptr(1));
-        uint8_t* out_base = reinterpret_cast<uint8_t*>(ptr(3));
-        const uint32_t* in_off = reinterpret_cast<const uint32_t*>(ptr(5));
-        const uint32_t* out_off = reinterpret_cast<const uint32_t*>(ptr(7));
-        uint32_t* out_len = reinterpret_cast<uint32_t*>(ptr(9));
-        uint8_t* status = reinterpret_cast<uint8_t*>(ptr(11));
+        const HPK_GAS uint8_t* in_base = gas(reinterpret_cast<const uint8_t*>(ptr(1)));
+        HPK_GAS uint8_t* out_base = gas(reinterpret_cast<uint8_t*>(ptr(3)));
+        const HPK_GAS uint32_t* in_off = gas(reinterpret_cast<const uint32_t*>(ptr(5)));
+        const HPK_GAS uint32_t* out_off = gas(reinterpret_cast<const uint32_t*>(ptr(7)));
+        HPK_GAS uint32_t* out_len = gas(reinterpret_cast<uint32_t*>(ptr(9)));
+        HPK_GAS uint8_t* status = gas(reinterpret_cast<uint8_t*>(ptr(11)));
         const uint32_t n = s_cmd[13], in_mis = s_cmd[14], out_mis = s_cmd[15], in_cap = s_cmd[16], out_cap = s_cmd[17];
         __syncthreads();  // (every thread has read s_cmd before wave 0 writes the next command)
         const uint32_t in_end = (n ? min(in_off[n], in_cap) : 0u) + in_mis;
         const uint32_t last16 = in_end ? (in_end - 1u) >> 4 : 0u;
-        const uint4* const g16 = reinterpret_cast<const uint4*>(in_base);
-        auto ld16 = [&](uint32_t ci) { return g16[min(ci, last16)]; };
+        const HPK_GAS u32x4* const g16 = reinterpret_cast<const HPK_GAS u32x4*>(in_base);
+        auto ld16 = [&](uint32_t ci) {
+            const u32x4 v = g16[min(ci, last16)];
+            return make_uint4(v.x, v.y, v.z, v.w);
+        };
         bool bad = false;
+        uint64_t tlv[4] = {0, 0, 0, 0};
+        const uint64_t tcmd = __builtin_amdgcn_s_memtime();
         for (uint32_t i = wg * kThreads + tid; i < n; i += G * kThreads) {
             const uint32_t p0 = in_off[i], p1 = in_off[i + 1], o0 = out_off[i], o1 = out_off[i + 1];
+            if (i == 0u) tlv[0] = __builtin_amdgcn_s_memtime() + (uint64_t)(p0 & 0u);
             if (!(p0 <= p1 && p1 <= in_cap && o0 <= o1 && o1 <= out_cap)) {
                 bad = true;
                 continue;
             }
             uint32_t cnt, st;
             const uint32_t b0 = p0 + in_mis;
-            if (((b0 + (p1 - p0) + 15u) >> 4) - (b0 >> 4) <= kPersistSlotChunks)
-                persist_literal_lds<kThreads>(g16, last16, s_slot + tid, s_lut, s_lo, out_base, out_mis, in_mis, p0, p1, o0,
-                                              o1, cnt, st);
+            if (((b0 + (p1 - p0) + 15u) >> 4) - (b0 >> 4) <= kPersistSlotChunks && p1 - p0 <= kPersistSlotMax)
+                persist_literal_lds<kThreads>(g16, last16, s_slot + kPersistInStride * tid,
+                                              reinterpret_cast<uint8_t*>(s_oslot + kPersistOutDw * tid), s_lut, s_lo,
+                                              out_base, out_mis, in_mis, p0, p1, o0, o1, cnt, st, i == 0u ? tlv : nullptr);
             else  // (a longer literal: walked from global memory)
                 persist_literal(ld16, s_lut, s_lo, out_base, out_mis, in_mis, p0, p1, o0, o1, cnt, st);
             out_len[i] = cnt;
             status[i] = (uint8_t)st;
+        }
+        if (wg == 0 && tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ctl->tl[k] = (uint32_t)(tlv[k] - (k ? tlv[k - 1] : tcmd));
         }
         if (bad) __hip_atomic_store(&p.dev[2], cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         served += 1u;

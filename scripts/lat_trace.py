@@ -46,7 +46,7 @@ def main():
             assert fn(*args) == 0
         ts = []
         dv = []  # (small-call mode) the device stamps' intervals, us
-        st4 = (ctypes.c_uint32 * 6)()
+        st4 = (ctypes.c_uint32 * 10)()
         for _ in range(reps):
             t0 = time.perf_counter()
             fn(*args)
@@ -54,7 +54,7 @@ def main():
             if small:
                 L.hpk_test_small_stamps(codec._h, st4)
                 dv.append([((st4[k + 1] - st4[k]) & 0xFFFFFFFF) / 100.0 for k in range(3)] +
-                          [st4[4] / max(st4[5], 1) * 0.1])  # shader clock, GHz
+                          [st4[4] / max(st4[5], 1) * 0.1] + [st4[6 + k] / 2400.0 for k in range(4)])  # GHz; us
         assert not st.any().item()
         assert torch.equal(ol.to(torch.int64), (w.dec_off[1 : n + 1] - w.dec_off[:n]).to(torch.int64))
         res.append({"lib": os.path.basename(os.environ.get("HPK_LIB", "libhpk.so")), "small_mode": small or None,
@@ -63,7 +63,8 @@ def main():
                     "p10_us": round(sorted(ts)[reps // 10] * 1e6, 1), "p90_us": round(sorted(ts)[reps * 9 // 10] * 1e6, 1)})
         if dv:
             res[-1]["device_us_median"] = {k: round(statistics.median(x[i] for x in dv), 2)
-                                           for i, k in enumerate(("broadcast", "decode_wg0", "last_publish", "sclk_ghz"))}
+                                           for i, k in enumerate(("broadcast", "decode_wg0", "last_publish", "sclk_ghz",
+                                                                      "lit0_offsets", "lit0_staged", "lit0_walk", "lit0_stores"))}
     for r in res:
         print(json.dumps(r), flush=True)
 
