@@ -669,7 +669,9 @@ int hpk_launch_encode(hpk_ctx* c, const hpk_batch& b) {
     // per = workgroups per CU; fewer when the batch is small (>= ~64 literals per workgroup)
     const int per = cfg == 1 ? 1 : 2;
     uint64_t blocks = ((uint64_t)b.n + 63) / 64;
-    if (blocks > (uint64_t)c->num_cu * per) blocks = (uint64_t)c->num_cu * per;
+    // (the small-call mode's persistent workgroups hold sm_wgs CUs, hpk_persist.h: left out of the grid)
+    const uint64_t cus = (uint64_t)c->num_cu - (c->sm_launched && c->sm_max ? (uint64_t)c->sm_wgs : 0u);
+    if (blocks > cus * per) blocks = cus * per;
     if (blocks < 1) blocks = 1;
     const dim3 grid((uint32_t)blocks);
     switch (cfg) {
