@@ -331,6 +331,54 @@ def run_host_inclusive(codec, w, reps=10):
     return res
 
 
+def run_small_calls(codec, w, n=1000, reps=200):
+    """Small synchronous calls at the granularity loona's read_headers decodes (one connection's block at a
+    time, crates/loona/src/h2/server.rs:1619-1637): the raw C call hpk_decode_batch on n device-resident
+    config-2 literals, synchronous, median and p10 over `reps` calls after 20 warm ones, through the launch
+    path and through the small-call mode (hpk_ctx_set_small_mode: a persistent kernel of 4 workgroups behind
+    a host-mapped doorbell). Lengths and statuses checked after each mode. Never `value`."""
+    import ctypes
+    import statistics
+
+    import torch
+
+    from loona_amd import _lib
+    from loona_amd.batch import decode_offsets_torch
+
+    L = _lib.lib()
+    io = w.enc_off[: n + 1].contiguous()
+    blob = w.enc_blob
+    oo = decode_offsets_torch(io)
+    out = torch.empty(int(oo[-1].item()) + 16, dtype=torch.uint8, device=blob.device)
+    ol = torch.empty(n, dtype=torch.int32, device=blob.device)
+    st = torch.empty(n, dtype=torch.uint8, device=blob.device)
+    want = (w.dec_off[1 : n + 1] - w.dec_off[:n]).to(torch.int64)
+    torch.cuda.synchronize()
+    args = (codec._h, ctypes.c_void_p(blob.data_ptr()), blob.numel(), ctypes.c_void_p(io.data_ptr()), ctypes.c_uint32(n),
+            ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.c_void_p(oo.data_ptr()), ctypes.c_void_p(ol.data_ptr()),
+            ctypes.c_void_p(st.data_ptr()), _lib.HPK_PTR_DEVICE)
+    res = {"literals": n, "calls": reps, "note": "raw C call, synchronous, device-resident config-2 literals"}
+    for mode in ("launch", "small_mode"):
+        if mode == "small_mode":
+            codec.set_small_mode(1024, 4, 50)
+        try:
+            for _ in range(20):
+                _lib.check(L.hpk_decode_batch(*args), "hpk_decode_batch")
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                L.hpk_decode_batch(*args)
+                ts.append(time.perf_counter() - t0)
+            ok = bool(torch.equal(ol.to(torch.int64), want)) and not bool(st.any().item())
+        finally:
+            if mode == "small_mode":
+                codec.set_small_mode(0)
+        ts.sort()
+        res[mode] = {"median_us": round(statistics.median(ts) * 1e6, 1), "p10_us": round(ts[reps // 10] * 1e6, 1),
+                     "checked": ok}
+    return res
+
+
 def run_config3(codec, stream, dev, reps=10):
     """BASELINE config 3: 1M mixed literals (Zipf(1.1) lengths 8..4096, 5 % uniform bytes), device
     encode and device decode timed apart, each over `reps` back-to-back launches; the round trip is
@@ -708,6 +756,7 @@ def main():
             "traffic": pmc_traffic(os.path.join(args.pmc_dir, "pmc_config2.json"), "config2", w2.n, source_hash()),
             "note": "1M literals, 4 rotating input/output copies (> 256 MiB Infinity Cache), 100 launches"}
         line["host_inclusive"] = run_host_inclusive(codec, w2)
+        line["small_calls"] = run_small_calls(codec, w2)
         cpu_w = w2
     elif rank == 0:
         cpu_w = units[0][0]
