@@ -668,9 +668,9 @@ def main():
                 "read_algorithmic": int(rd_algo), "read_pmc": pm_hbm.get("read_bytes_per_launch"),
                 "write_algorithmic": int(wr_algo), "write_region_spans": int(wr_span),
                 "write_pmc": pm_hbm.get("write_bytes_per_launch"),
-                "why": "reads: every fill loads its whole 3 KiB window from a 16-B-aligned start, so the bytes "
-                       "past the fill's last literal are read again by the next fill, and in_off/out_off are "
-                       "read as (t, t+1) pairs; writes: the image write-back stores each fill's whole output span "
+                "why": "reads: a fill's window starts 16-B-aligned and runs to its chunk's end (lines shared by "
+                       "neighbouring chunks are read by both waves) and in_off/out_off are read as (t, t+1) "
+                       "pairs; writes: the image write-back stores each fill's whole output span "
                        "(the regions' slack between out_len and the 8/5 bound included) in 16-B chunks"}
         issue = None
         if pm_sq:
