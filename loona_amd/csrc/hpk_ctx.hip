@@ -5,7 +5,7 @@
 
 #include "hpk_device.h"
 
-#define HPK_VERSION "hpk 0.36 gfx950 decode v36 (every batch: wave fills, each wave with its own LDS window and image, longest-first queue, slot end offsets by DPP, nontemporal window loads stopping at the chunk's last byte, nontemporal write-back; chunks by guided self-scheduling from 4M literals, fixed 96-literal chunks below; fills and long-literal phase: body steps with no fit tests while >= 29 bits are left, then checked tails (the long phase's at its refill points); long literals one lane each streaming from HBM after the fills, dense ranges listed longest-first; literals of >= 8 KiB by a whole workgroup in speculative pieces; compacted-output form: wave fills packed per workgroup from an LDS cursor into a bound layout made from the input offsets, each lane storing its two literals in unaligned 16-byte pieces; small-call mode: a persistent kernel behind a host-mapped doorbell); encode v5 (byte-balanced workgroup ranges, start map and DPP segmented scan, run accumulator, LDS image, live chunks only)"
+#define HPK_VERSION "hpk 0.37 gfx950 decode v37 (every batch: wave fills, each wave with its own LDS window and image, longest-first queue, slot end offsets by DPP, nontemporal window loads stopping at the chunk's last byte, nontemporal write-back; chunks by guided self-scheduling from 4M literals, fixed 96-literal chunks below; fills and long-literal phase: body steps with no fit tests while >= 29 bits are left, then checked tails (the long phase's at its refill points); long literals one lane each streaming from HBM after the fills, dense ranges listed longest-first; literals of >= 8 KiB by a whole workgroup in speculative pieces; compacted-output form: wave fills packed per workgroup from an LDS cursor into a bound layout made from the input offsets, each lane storing its two literals in unaligned 16-byte pieces; small-call mode: a persistent kernel behind a host-mapped doorbell); encode v5 (byte-balanced workgroup ranges, start map and DPP segmented scan, run accumulator, LDS image, live chunks only)"
 
 static thread_local std::string t_last_error;
 

@@ -102,7 +102,7 @@ __device__ __forceinline__ void pin(uint32_t x) { asm volatile("" ::"v"(x)); }
 #endif
 
 #ifndef HPK_LONG_CH
-#define HPK_LONG_CH 2  // 16-byte chunks a lane loads per refill point
+#define HPK_LONG_CH 3  // 16-byte chunks a lane loads per refill point (round 6: 3, config 3 633.0-634.1 vs 641.7-642.4 us)
 #endif
 
 #ifndef HPK_LONG_OS
